@@ -1,0 +1,683 @@
+// gol_capi.cpp -- C ABI of libgol (include/gol.h): shard contexts, device
+// planes, the per-generation schedule (interior || RCCL halo exchange, then
+// boundary rows), hashing, snapshots, checkpoints and kernel timing.
+//
+// Reference correspondence (src/main/scala/gameoflife/ of the reference):
+//   gol_create   <- BoardCreator.createAllInitialActors (BoardCreator.scala:79-89)
+//   gol_seed     <- initialState = Random.nextBoolean() per cell (BoardCreator.scala:23)
+//   gol_step     <- NextStep tick -> CurrentEpochMsg -> gatherer -> SetNewStateMsg
+//                   (BoardCreator.scala:113-116, CellActor.scala:63-91,
+//                    NextStateCellGathererActor.scala:25-48)
+//   gol_snapshot <- CellStateMsg -> LoggerActor (CellActor.scala:89, LoggerActor.scala:30-46)
+//   gol_comm_*   <- cross-backend GetStateFromEpoch/StateForEpoch over Akka remote
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gol.h"
+#include "gol_kernels.h"
+
+namespace {
+
+std::mutex g_err_mu;
+std::string g_err;  // process-wide last error (gol_create failures)
+
+struct EventPair {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
+}  // namespace
+
+struct gol_ctx {
+    // geometry
+    int64_t width = 0, height = 0, row0 = 0, rows = 0;
+    int32_t wwords = 0;
+    int64_t pitch = 0;
+    int32_t topology = GOL_TORUS;
+    uint32_t birth = 0, survive = 0;
+    int64_t vis_w = 0, vis_h = 0;
+    int device = 0;
+    int vec = 1;
+    // device state
+    uint32_t* plane[2] = {nullptr, nullptr};
+    int cur = 0;
+    uint32_t* halo_top = nullptr;  // RCCL receive buffers (sharded)
+    uint32_t* halo_bot = nullptr;
+    uint32_t* zero_row = nullptr;
+    unsigned long long* slots = nullptr;  // [gens][kHashSlots * kHashSlotStride]
+    uint32_t slots_gens = 0;
+    std::vector<unsigned long long> host_slots;
+    uint64_t epoch = 0;
+    hipStream_t compute = nullptr, comm = nullptr;
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    // RCCL
+    ncclComm_t nccl = nullptr;
+    int rank = 0, nranks = 1;
+    // tuning
+    int32_t band_rows = 0, gens_per_pass = 1;
+    // profiling
+    bool prof = false;
+    std::vector<EventPair> evs;
+    size_t evs_used = 0;
+    double prof_ms = 0.0;
+    uint64_t prof_launches = 0;
+    std::string err;
+};
+
+namespace {
+
+int set_err(gol_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (ctx) {
+        ctx->err = buf;
+    } else {
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        g_err = buf;
+    }
+    return code;
+}
+
+#define HIP_CHECK(ctx, expr)                                                                      \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return set_err((ctx), GOL_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                           __FILE__, __LINE__);                                                   \
+    } while (0)
+
+#define NCCL_CHECK(ctx, expr)                                                                       \
+    do {                                                                                            \
+        ncclResult_t r_ = (expr);                                                                   \
+        if (r_ != ncclSuccess)                                                                      \
+            return set_err((ctx), GOL_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
+                           __FILE__, __LINE__);                                                     \
+    } while (0)
+
+bool sharded(const gol_ctx* c) { return c->nccl != nullptr && c->nranks > 1; }
+
+int bind(gol_ctx* ctx) {
+    HIP_CHECK(ctx, hipSetDevice(ctx->device));
+    return GOL_OK;
+}
+
+int ensure_slots(gol_ctx* ctx, uint32_t gens) {
+    if (gens <= ctx->slots_gens) return GOL_OK;
+    if (ctx->slots) HIP_CHECK(ctx, hipFree(ctx->slots));
+    ctx->slots = nullptr;
+    const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
+    HIP_CHECK(ctx, hipMalloc(&ctx->slots, n * sizeof(unsigned long long)));
+    ctx->slots_gens = gens;
+    ctx->host_slots.resize(n);
+    return GOL_OK;
+}
+
+// Sum the kHashSlots accumulators of each generation (mod 2^64).
+void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out) {
+    for (uint32_t g = 0; g < gens; ++g) {
+        uint64_t h = 0;
+        const unsigned long long* s =
+            ctx->host_slots.data() + (size_t)g * gol::kHashSlots * gol::kHashSlotStride;
+        for (int k = 0; k < gol::kHashSlots; ++k) h += s[(size_t)k * gol::kHashSlotStride];
+        out[g] = h;
+    }
+}
+
+EventPair* next_event_pair(gol_ctx* ctx);
+
+int fold_profile(gol_ctx* ctx) {
+    for (size_t i = 0; i < ctx->evs_used; ++i) {
+        HIP_CHECK(ctx, hipEventSynchronize(ctx->evs[i].stop));
+        float ms = 0.f;
+        HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->evs[i].start, ctx->evs[i].stop));
+        ctx->prof_ms += ms;
+        ctx->prof_launches += 1;
+    }
+    ctx->evs_used = 0;
+    return GOL_OK;
+}
+
+EventPair* next_event_pair(gol_ctx* ctx) {
+    constexpr size_t kMaxPairs = 4096;
+    if (ctx->evs_used == ctx->evs.size()) {
+        if (ctx->evs.size() >= kMaxPairs) {
+            if (fold_profile(ctx) != GOL_OK) return nullptr;
+        } else {
+            EventPair e;
+            if (hipEventCreate(&e.start) != hipSuccess || hipEventCreate(&e.stop) != hipSuccess)
+                return nullptr;
+            ctx->evs.push_back(e);
+        }
+    }
+    return &ctx->evs[ctx->evs_used++];
+}
+
+int pick_band(const gol_ctx* ctx, int64_t rows, int strips) {
+    if (ctx->band_rows > 0) return ctx->band_rows;
+    // Aim at ~8192 waves: one full residency round of 256-thread workgroups
+    // (8 per CU x 256 CUs x 4 waves) so all bands finish together.
+    const int64_t target_waves = 8192;
+    int64_t bands = std::max<int64_t>(1, target_waves / std::max(1, strips));
+    int64_t band = (rows + bands - 1) / bands;
+    band = std::max<int64_t>(band, 8);
+    band = std::min<int64_t>(band, 4096);
+    return (int)band;
+}
+
+// Launch the step kernel over local row ranges [lo0,hi0) (+ [lo1,hi1) if n==2).
+// Only the main launch of a generation (whole shard, or the interior rows of
+// a sharded shard) is bracketed by profiling events: it is the dominant kernel.
+int launch_ranges(gol_ctx* ctx, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
+                  const uint32_t* hbot, unsigned long long* slots, int n, const int32_t* lo,
+                  const int32_t* hi, bool main_launch) {
+    gol::StepParams p{};
+    p.cur = cur;
+    p.nxt = nxt;
+    p.halo_top = htop;
+    p.halo_bot = hbot;
+    p.hash_slots = slots;
+    p.pitch = ctx->pitch;
+    p.grow0 = ctx->row0;
+    p.vis_rows = ctx->topology == GOL_TORUS ? ctx->height : ctx->vis_h;
+    p.vis_cols = ctx->topology == GOL_TORUS ? ctx->width : ctx->vis_w;
+    p.width = ctx->width;
+    p.wwords = ctx->wwords;
+    p.rows = (int32_t)ctx->rows;
+    p.strips = (int32_t)((ctx->wwords + gol::kWaveLanes * ctx->vec - 1) / (gol::kWaveLanes * ctx->vec));
+    int64_t maxlen = 0;
+    for (int k = 0; k < n; ++k) maxlen = std::max<int64_t>(maxlen, hi[k] - lo[k]);
+    p.band = pick_band(ctx, maxlen, p.strips);
+    int maxbands = 0;
+    for (int k = 0; k < 2; ++k) {
+        if (k < n) {
+            p.row_lo[k] = lo[k];
+            p.row_hi[k] = hi[k];
+            p.nbands[k] = (hi[k] - lo[k] + p.band - 1) / p.band;
+        } else {
+            p.row_lo[k] = p.row_hi[k] = p.nbands[k] = 0;
+        }
+        maxbands = std::max(maxbands, p.nbands[k]);
+    }
+    if (maxbands == 0) return GOL_OK;
+    p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
+    p.birth = ctx->birth;
+    p.survive = ctx->survive;
+    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
+    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
+    const int64_t waves = (int64_t)p.strips * maxbands;
+    const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
+    EventPair* ev = nullptr;
+    if (ctx->prof && main_launch) {
+        ev = next_event_pair(ctx);
+        if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
+        HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
+    }
+    HIP_CHECK(ctx, gol::launch_step(p, ctx->vec, life, slots != nullptr, clipped, gx, n, ctx->compute));
+    if (ev) HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
+    return GOL_OK;
+}
+
+// One generation.  slots: this generation's hash accumulators or null.
+int one_generation(gol_ctx* ctx, unsigned long long* slots) {
+    uint32_t* cur = ctx->plane[ctx->cur];
+    uint32_t* nxt = ctx->plane[ctx->cur ^ 1];
+    const int32_t rows = (int32_t)ctx->rows;
+    const bool torus = ctx->topology == GOL_TORUS;
+    if (!sharded(ctx)) {
+        const uint32_t* htop = torus ? cur + (int64_t)(rows - 1) * ctx->pitch : ctx->zero_row;
+        const uint32_t* hbot = torus ? cur : ctx->zero_row;
+        const int32_t lo[1] = {0}, hi[1] = {rows};
+        int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+        if (rc) return rc;
+    } else {
+        const int up = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
+        const int down = (ctx->rank + 1) % ctx->nranks;
+        const bool has_up = torus || ctx->rank > 0;
+        const bool has_down = torus || ctx->rank < ctx->nranks - 1;
+        // Halo exchange on the comm stream once the current plane is final.
+        HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
+        HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
+        NCCL_CHECK(ctx, ncclGroupStart());
+        // Issue order matters when up == down (2 ranks): per-peer FIFO matching
+        // pairs my last row with the peer's top halo and my first row with its
+        // bottom halo.
+        if (has_down)
+            NCCL_CHECK(ctx, ncclSend(cur + (int64_t)(rows - 1) * ctx->pitch, ctx->wwords, ncclUint32, down,
+                                     ctx->nccl, ctx->comm));
+        if (has_up) NCCL_CHECK(ctx, ncclSend(cur, ctx->wwords, ncclUint32, up, ctx->nccl, ctx->comm));
+        if (has_up) NCCL_CHECK(ctx, ncclRecv(ctx->halo_top, ctx->wwords, ncclUint32, up, ctx->nccl, ctx->comm));
+        if (has_down)
+            NCCL_CHECK(ctx, ncclRecv(ctx->halo_bot, ctx->wwords, ncclUint32, down, ctx->nccl, ctx->comm));
+        NCCL_CHECK(ctx, ncclGroupEnd());
+        HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
+        const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
+        const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
+        if (rows > 2) {
+            // interior rows overlap the exchange; boundary rows follow it
+            const int32_t lo[1] = {1}, hi[1] = {rows - 1};
+            int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+            if (rc) return rc;
+            HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
+            const int32_t blo[2] = {0, rows - 1}, bhi[2] = {1, rows};
+            rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 2, blo, bhi, false);
+            if (rc) return rc;
+        } else {
+            HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
+            const int32_t lo[1] = {0}, hi[1] = {rows};
+            int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+            if (rc) return rc;
+        }
+    }
+    ctx->cur ^= 1;
+    ctx->epoch += 1;
+    return GOL_OK;
+}
+
+void destroy_impl(gol_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->compute) hipStreamSynchronize(c->compute);
+    if (c->comm) hipStreamSynchronize(c->comm);
+    if (c->nccl) ncclCommDestroy(c->nccl);
+    for (auto& e : c->evs) {
+        if (e.start) hipEventDestroy(e.start);
+        if (e.stop) hipEventDestroy(e.stop);
+    }
+    if (c->ev_ready) hipEventDestroy(c->ev_ready);
+    if (c->ev_halo) hipEventDestroy(c->ev_halo);
+    for (auto* p : c->plane) if (p) hipFree(p);
+    if (c->halo_top) hipFree(c->halo_top);
+    if (c->halo_bot) hipFree(c->halo_bot);
+    if (c->zero_row) hipFree(c->zero_row);
+    if (c->slots) hipFree(c->slots);
+    if (c->compute) hipStreamDestroy(c->compute);
+    if (c->comm) hipStreamDestroy(c->comm);
+    delete c;
+}
+
+struct CkptHeader {
+    char magic[8];  // "GOLCKPT1"
+    int64_t width, height, row0, rows;
+    int64_t wwords;
+    uint64_t epoch;
+    int32_t topology;
+    uint32_t birth, survive;
+    int32_t pad;
+};
+
+}  // namespace
+
+extern "C" {
+
+int gol_abi_version(void) { return GOL_ABI_VERSION; }
+
+const char* gol_strerror(int code) {
+    switch (code) {
+        case GOL_OK: return "ok";
+        case GOL_EINVAL: return "invalid argument";
+        case GOL_EHIP: return "HIP runtime error";
+        case GOL_ENOMEM: return "out of memory";
+        case GOL_ECOMM: return "communication (RCCL) error";
+        case GOL_ESTATE: return "invalid state";
+        case GOL_ENODEV: return "no HIP device";
+        default: return "unknown error";
+    }
+}
+
+const char* gol_last_error(const gol_ctx* ctx) {
+    if (ctx) return ctx->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    static thread_local std::string copy;
+    copy = g_err;
+    return copy.c_str();
+}
+
+int gol_device_count(int* count) {
+    if (!count) return set_err(nullptr, GOL_EINVAL, "count is null");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return GOL_OK;
+}
+
+int gol_shard_rows(int64_t height, int rank, int nranks, int64_t* row0, int64_t* rows) {
+    if (height <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || !row0 || !rows)
+        return set_err(nullptr, GOL_EINVAL, "gol_shard_rows: bad arguments");
+    if (height < nranks) return set_err(nullptr, GOL_EINVAL, "gol_shard_rows: fewer rows than ranks");
+    // contiguous blocks; the first (height % nranks) ranks get one extra row
+    const int64_t base = height / nranks, extra = height % nranks;
+    *row0 = rank * base + std::min<int64_t>(rank, extra);
+    *rows = base + (rank < extra ? 1 : 0);
+    return GOL_OK;
+}
+
+int gol_create(gol_ctx** out, const gol_config* cfg) {
+    if (!out || !cfg) return set_err(nullptr, GOL_EINVAL, "gol_create: null argument");
+    *out = nullptr;
+    const gol_config& c = *cfg;
+    if (c.width <= 0 || c.height <= 0) return set_err(nullptr, GOL_EINVAL, "width/height must be > 0");
+    if (c.topology != GOL_TORUS && c.topology != GOL_REF_CLIPPED)
+        return set_err(nullptr, GOL_EINVAL, "unknown topology %d", c.topology);
+    if (c.topology == GOL_TORUS && c.width % 32 != 0)
+        return set_err(nullptr, GOL_EINVAL, "torus width must be a multiple of 32 (got %lld)", (long long)c.width);
+    if ((c.birth_mask | c.survive_mask) & ~0x1FFu)
+        return set_err(nullptr, GOL_EINVAL, "rule masks must fit in 9 bits");
+    const int64_t rows = c.rows > 0 ? c.rows : c.height - c.row0;
+    if (c.row0 < 0 || rows <= 0 || c.row0 + rows > c.height)
+        return set_err(nullptr, GOL_EINVAL, "shard rows [%lld, %lld) outside the board", (long long)c.row0,
+                       (long long)(c.row0 + rows));
+    const int64_t wwords = (c.width + 31) / 32;
+    if (wwords > (1 << 30) || rows > (1 << 30))
+        return set_err(nullptr, GOL_EINVAL, "board too large");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(nullptr, GOL_ENODEV, "no HIP device available (libgol has no CPU fallback)");
+    if (c.device < 0 || c.device >= ndev)
+        return set_err(nullptr, GOL_EINVAL, "device %d out of range (%d devices)", c.device, ndev);
+
+    gol_ctx* ctx = new gol_ctx();
+    ctx->width = c.width;
+    ctx->height = c.height;
+    ctx->row0 = c.row0;
+    ctx->rows = rows;
+    ctx->wwords = (int32_t)wwords;
+    ctx->pitch = (wwords + 63) / 64 * 64;  // 256-byte aligned rows
+    ctx->topology = c.topology;
+    ctx->birth = c.birth_mask;
+    ctx->survive = c.survive_mask;
+    ctx->vis_w = c.vis_width > 0 ? c.vis_width : c.width - 1;
+    ctx->vis_h = c.vis_height > 0 ? c.vis_height : c.height - 1;
+    ctx->device = c.device;
+    ctx->vec = (wwords % 4 == 0 && wwords >= 256) ? 4 : (wwords % 2 == 0 && wwords >= 128) ? 2 : 1;
+
+    auto fail = [&](int rc) {
+        std::string msg = ctx->err;
+        destroy_impl(ctx);
+        set_err(nullptr, rc, "%s", msg.c_str());
+        return rc;
+    };
+    if (bind(ctx)) return fail(GOL_EHIP);
+    const size_t plane_bytes = (size_t)rows * ctx->pitch * sizeof(uint32_t);
+    for (int k = 0; k < 2; ++k) {
+        if (hipMalloc(&ctx->plane[k], plane_bytes) != hipSuccess) {
+            set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes failed", plane_bytes);
+            return fail(GOL_ENOMEM);
+        }
+        if (hipMemset(ctx->plane[k], 0, plane_bytes) != hipSuccess) {
+            set_err(ctx, GOL_EHIP, "hipMemset failed");
+            return fail(GOL_EHIP);
+        }
+    }
+    const size_t row_bytes = (size_t)ctx->pitch * sizeof(uint32_t);
+    if (hipMalloc(&ctx->halo_top, row_bytes) != hipSuccess || hipMalloc(&ctx->halo_bot, row_bytes) != hipSuccess ||
+        hipMalloc(&ctx->zero_row, row_bytes) != hipSuccess) {
+        set_err(ctx, GOL_ENOMEM, "halo allocation failed");
+        return fail(GOL_ENOMEM);
+    }
+    if (hipMemset(ctx->halo_top, 0, row_bytes) != hipSuccess || hipMemset(ctx->halo_bot, 0, row_bytes) != hipSuccess ||
+        hipMemset(ctx->zero_row, 0, row_bytes) != hipSuccess) {
+        set_err(ctx, GOL_EHIP, "hipMemset failed");
+        return fail(GOL_EHIP);
+    }
+    if (hipStreamCreateWithFlags(&ctx->compute, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->comm, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_halo, hipEventDisableTiming) != hipSuccess) {
+        set_err(ctx, GOL_EHIP, "stream/event creation failed");
+        return fail(GOL_EHIP);
+    }
+    if (hipDeviceSynchronize() != hipSuccess) {
+        set_err(ctx, GOL_EHIP, "hipDeviceSynchronize failed");
+        return fail(GOL_EHIP);
+    }
+    *out = ctx;
+    return GOL_OK;
+}
+
+void gol_destroy(gol_ctx* ctx) { destroy_impl(ctx); }
+
+int gol_seed(gol_ctx* ctx, uint64_t seed) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (int rc = bind(ctx)) return rc;
+    HIP_CHECK(ctx, gol::launch_seed(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->width, ctx->row0,
+                                    (int32_t)ctx->rows, seed, ctx->compute));
+    ctx->epoch = 0;
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    return GOL_OK;
+}
+
+int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words) {
+    if (!ctx || !packed) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (host_pitch_words < ctx->wwords)
+        return set_err(ctx, GOL_EINVAL, "host pitch %lld < words per row %d", (long long)host_pitch_words,
+                       ctx->wwords);
+    // Bits beyond the board width must be dead (layout invariant).
+    if (ctx->width % 32) {
+        const uint32_t m = (uint32_t)((1ull << (ctx->width % 32)) - 1ull);
+        for (int64_t r = 0; r < ctx->rows; ++r)
+            if (packed[r * host_pitch_words + ctx->wwords - 1] & ~m)
+                return set_err(ctx, GOL_EINVAL, "padding bits beyond width set in row %lld", (long long)r);
+    }
+    if (int rc = bind(ctx)) return rc;
+    HIP_CHECK(ctx, hipMemcpy2DAsync(ctx->plane[ctx->cur], ctx->pitch * 4, packed, host_pitch_words * 4,
+                                    (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyHostToDevice, ctx->compute));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    ctx->epoch = 0;
+    return GOL_OK;
+}
+
+int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (int rc = bind(ctx)) return rc;
+    if (generations == 0) return GOL_OK;
+    if (!hashes_out) {
+        for (uint32_t g = 0; g < generations; ++g)
+            if (int rc = one_generation(ctx, nullptr)) return rc;
+        return GOL_OK;
+    }
+    constexpr uint32_t kChunk = 1024;
+    for (uint32_t g0 = 0; g0 < generations; g0 += kChunk) {
+        const uint32_t n = std::min(kChunk, generations - g0);
+        if (int rc = ensure_slots(ctx, n)) return rc;
+        const size_t per = (size_t)gol::kHashSlots * gol::kHashSlotStride;
+        HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, n * per * sizeof(unsigned long long), ctx->compute));
+        for (uint32_t g = 0; g < n; ++g)
+            if (int rc = one_generation(ctx, ctx->slots + g * per)) return rc;
+        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, n * per * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, ctx->compute));
+        HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+        fold_slots(ctx, n, hashes_out + g0);
+    }
+    return GOL_OK;
+}
+
+int gol_epoch(const gol_ctx* ctx, uint64_t* epoch) {
+    if (!ctx || !epoch) return set_err(nullptr, GOL_EINVAL, "null argument");
+    *epoch = ctx->epoch;
+    return GOL_OK;
+}
+
+int gol_sync(gol_ctx* ctx) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (int rc = bind(ctx)) return rc;
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->comm));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    return GOL_OK;
+}
+
+int gol_hash(gol_ctx* ctx, uint64_t* hash_out) {
+    if (!ctx || !hash_out) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (int rc = bind(ctx)) return rc;
+    if (int rc = ensure_slots(ctx, 1)) return rc;
+    const size_t per = (size_t)gol::kHashSlots * gol::kHashSlotStride;
+    HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, per * sizeof(unsigned long long), ctx->compute));
+    HIP_CHECK(ctx, gol::launch_hash(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
+                                    ctx->slots, ctx->compute));
+    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, per * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, ctx->compute));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    fold_slots(ctx, 1, hash_out);
+    return GOL_OK;
+}
+
+int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words) {
+    if (!ctx || !packed_out) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (host_pitch_words < ctx->wwords) return set_err(ctx, GOL_EINVAL, "host pitch too small");
+    if (int rc = bind(ctx)) return rc;
+    HIP_CHECK(ctx, hipMemcpy2DAsync(packed_out, host_pitch_words * 4, ctx->plane[ctx->cur], ctx->pitch * 4,
+                                    (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyDeviceToHost, ctx->compute));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    return GOL_OK;
+}
+
+int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state) {
+    if (!ctx || !state) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (x < 0 || x >= ctx->width || y < ctx->row0 || y >= ctx->row0 + ctx->rows)
+        return set_err(ctx, GOL_EINVAL, "cell (%lld, %lld) not in this shard", (long long)x, (long long)y);
+    if (int rc = bind(ctx)) return rc;
+    uint32_t w = 0;
+    HIP_CHECK(ctx, hipMemcpyAsync(&w, ctx->plane[ctx->cur] + (y - ctx->row0) * ctx->pitch + x / 32, 4,
+                                  hipMemcpyDeviceToHost, ctx->compute));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    *state = (int)((w >> (x % 32)) & 1u);
+    return GOL_OK;
+}
+
+int gol_checkpoint_bytes(const gol_ctx* ctx, size_t* bytes) {
+    if (!ctx || !bytes) return set_err(nullptr, GOL_EINVAL, "null argument");
+    *bytes = sizeof(CkptHeader) + (size_t)ctx->rows * ctx->wwords * sizeof(uint32_t);
+    return GOL_OK;
+}
+
+int gol_checkpoint(gol_ctx* ctx, void* host_out, size_t bytes) {
+    size_t need = 0;
+    if (!ctx || !host_out) return set_err(ctx, GOL_EINVAL, "null argument");
+    gol_checkpoint_bytes(ctx, &need);
+    if (bytes < need) return set_err(ctx, GOL_EINVAL, "checkpoint buffer too small (%zu < %zu)", bytes, need);
+    CkptHeader h{};
+    memcpy(h.magic, "GOLCKPT1", 8);
+    h.width = ctx->width; h.height = ctx->height; h.row0 = ctx->row0; h.rows = ctx->rows;
+    h.wwords = ctx->wwords; h.epoch = ctx->epoch; h.topology = ctx->topology;
+    h.birth = ctx->birth; h.survive = ctx->survive;
+    memcpy(host_out, &h, sizeof h);
+    return gol_snapshot(ctx, reinterpret_cast<uint32_t*>(static_cast<char*>(host_out) + sizeof h), ctx->wwords);
+}
+
+int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes) {
+    if (!ctx || !host_in) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (bytes < sizeof(CkptHeader)) return set_err(ctx, GOL_EINVAL, "checkpoint truncated");
+    CkptHeader h;
+    memcpy(&h, host_in, sizeof h);
+    if (memcmp(h.magic, "GOLCKPT1", 8) != 0) return set_err(ctx, GOL_EINVAL, "bad checkpoint magic");
+    if (h.width != ctx->width || h.height != ctx->height || h.row0 != ctx->row0 || h.rows != ctx->rows ||
+        h.topology != ctx->topology || h.birth != ctx->birth || h.survive != ctx->survive)
+        return set_err(ctx, GOL_EINVAL, "checkpoint geometry/rule does not match this context");
+    if (bytes < sizeof h + (size_t)h.rows * h.wwords * 4) return set_err(ctx, GOL_EINVAL, "checkpoint truncated");
+    int rc = gol_load(ctx, reinterpret_cast<const uint32_t*>(static_cast<const char*>(host_in) + sizeof h), h.wwords);
+    if (rc) return rc;
+    ctx->epoch = h.epoch;
+    return GOL_OK;
+}
+
+int gol_comm_unique_id(uint8_t id_out[GOL_UNIQUE_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) == GOL_UNIQUE_ID_BYTES, "ncclUniqueId size");
+    if (!id_out) return set_err(nullptr, GOL_EINVAL, "null argument");
+    ncclUniqueId id;
+    NCCL_CHECK(nullptr, ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof id);
+    return GOL_OK;
+}
+
+int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank, int nranks) {
+    if (!ctx || !id) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, GOL_EINVAL, "bad rank/nranks");
+    if (ctx->nccl) return set_err(ctx, GOL_ESTATE, "communicator already initialised");
+    if (int rc = bind(ctx)) return rc;
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof uid);
+    NCCL_CHECK(ctx, ncclCommInitRank(&ctx->nccl, nranks, uid, rank));
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return GOL_OK;
+}
+
+int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count) {
+    if (!ctx || (!values && count)) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (!ctx->nccl) return set_err(ctx, GOL_ECOMM, "no communicator (call gol_comm_init)");
+    if (count == 0) return GOL_OK;
+    if (int rc = bind(ctx)) return rc;
+    uint64_t* d = nullptr;
+    HIP_CHECK(ctx, hipMallocAsync((void**)&d, count * sizeof(uint64_t), ctx->comm));
+    HIP_CHECK(ctx, hipMemcpyAsync(d, values, count * sizeof(uint64_t), hipMemcpyHostToDevice, ctx->comm));
+    NCCL_CHECK(ctx, ncclAllReduce(d, d, count, ncclUint64, ncclSum, ctx->nccl, ctx->comm));
+    HIP_CHECK(ctx, hipMemcpyAsync(values, d, count * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->comm));
+    HIP_CHECK(ctx, hipFreeAsync(d, ctx->comm));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->comm));
+    return GOL_OK;
+}
+
+int gol_profile_enable(gol_ctx* ctx, int enable) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    ctx->prof = enable != 0;
+    return GOL_OK;
+}
+
+int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (int rc = bind(ctx)) return rc;
+    if (int rc = fold_profile(ctx)) return rc;
+    if (total_ms) *total_ms = ctx->prof_ms;
+    if (launches) *launches = ctx->prof_launches;
+    return GOL_OK;
+}
+
+int gol_profile_reset(gol_ctx* ctx) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (int rc = bind(ctx)) return rc;
+    if (int rc = fold_profile(ctx)) return rc;
+    ctx->prof_ms = 0.0;
+    ctx->prof_launches = 0;
+    return GOL_OK;
+}
+
+int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (band_rows < 0 || gens_per_pass < 0) return set_err(ctx, GOL_EINVAL, "negative tuning value");
+    ctx->band_rows = band_rows;
+    ctx->gens_per_pass = gens_per_pass > 0 ? gens_per_pass : 1;
+    if (ctx->gens_per_pass != 1) return set_err(ctx, GOL_EINVAL, "gens_per_pass > 1 not available yet");
+    return GOL_OK;
+}
+
+int gol_selftest(int device, uint32_t* report) {
+    // report[256]: see gol::selftest_kernel.  Diagnoses the DPP wave shifts,
+    // v_alignbit and SMEM loads the step kernel relies on.
+    if (!report) return set_err(nullptr, GOL_EINVAL, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return set_err(nullptr, GOL_ENODEV, "no HIP device available");
+    HIP_CHECK(nullptr, hipSetDevice(device));
+    uint32_t h_in[64];
+    for (int i = 0; i < 64; ++i) h_in[i] = 0x01000193u * (uint32_t)(i + 1) ^ (uint32_t)(i << 24);
+    uint32_t *d_in = nullptr, *d_out = nullptr;
+    HIP_CHECK(nullptr, hipMalloc(&d_in, sizeof h_in));
+    HIP_CHECK(nullptr, hipMalloc(&d_out, 256 * sizeof(uint32_t)));
+    HIP_CHECK(nullptr, hipMemcpy(d_in, h_in, sizeof h_in, hipMemcpyHostToDevice));
+    HIP_CHECK(nullptr, gol::launch_selftest(d_in, d_out, nullptr));
+    HIP_CHECK(nullptr, hipMemcpy(report, d_out, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    hipFree(d_in);
+    hipFree(d_out);
+    return GOL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+"""ctypes binding of libgol.so (include/gol.h).
+
+The product path: every call goes to the HIP library.  If the library is not
+built, importing this module raises immediately -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgol.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "gol.h")
+
+GOL_OK = 0
+GOL_EINVAL = 1
+GOL_EHIP = 2
+GOL_ENOMEM = 3
+GOL_ECOMM = 4
+GOL_ESTATE = 5
+GOL_ENODEV = 6
+
+GOL_TORUS = 0
+GOL_REF_CLIPPED = 1
+GOL_UNIQUE_ID_BYTES = 128
+
+
+class GolError(RuntimeError):
+    """A nonzero libgol return code (the analogue of the exception a cell
+    actor throws, which the reference's supervisor turns into a Restart,
+    BoardCreator.scala:42-45)."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"libgol error {code} ({_strerror(code)}): {message}")
+        self.code = code
+        self.message = message
+
+
+class GolConfig(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int64),
+        ("height", ctypes.c_int64),
+        ("row0", ctypes.c_int64),
+        ("rows", ctypes.c_int64),
+        ("topology", ctypes.c_int32),
+        ("birth_mask", ctypes.c_uint32),
+        ("survive_mask", ctypes.c_uint32),
+        ("device", ctypes.c_int32),
+        ("vis_width", ctypes.c_int64),
+        ("vis_height", ctypes.c_int64),
+    ]
+
+
+_c = ctypes
+_vp = ctypes.c_void_p
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+_SIGNATURES = {
+    "gol_abi_version": (_c.c_int, []),
+    "gol_strerror": (_c.c_char_p, [_c.c_int]),
+    "gol_last_error": (_c.c_char_p, [_vp]),
+    "gol_device_count": (_c.c_int, [ctypes.POINTER(_c.c_int)]),
+    "gol_shard_rows": (_c.c_int, [_c.c_int64, _c.c_int, _c.c_int, ctypes.POINTER(_c.c_int64),
+                                  ctypes.POINTER(_c.c_int64)]),
+    "gol_create": (_c.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(GolConfig)]),
+    "gol_destroy": (None, [_vp]),
+    "gol_seed": (_c.c_int, [_vp, _c.c_uint64]),
+    "gol_load": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_step": (_c.c_int, [_vp, _c.c_uint32, _u64p]),
+    "gol_epoch": (_c.c_int, [_vp, _u64p]),
+    "gol_sync": (_c.c_int, [_vp]),
+    "gol_hash": (_c.c_int, [_vp, _u64p]),
+    "gol_snapshot": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_get_cell": (_c.c_int, [_vp, _c.c_int64, _c.c_int64, ctypes.POINTER(_c.c_int)]),
+    "gol_checkpoint_bytes": (_c.c_int, [_vp, ctypes.POINTER(_c.c_size_t)]),
+    "gol_checkpoint": (_c.c_int, [_vp, _vp, _c.c_size_t]),
+    "gol_restore": (_c.c_int, [_vp, _vp, _c.c_size_t]),
+    "gol_comm_unique_id": (_c.c_int, [_u8p]),
+    "gol_comm_init": (_c.c_int, [_vp, _u8p, _c.c_int, _c.c_int]),
+    "gol_comm_allreduce_u64": (_c.c_int, [_vp, _u64p, _c.c_uint32]),
+    "gol_profile_enable": (_c.c_int, [_vp, _c.c_int]),
+    "gol_profile_read": (_c.c_int, [_vp, ctypes.POINTER(_c.c_double), _u64p]),
+    "gol_profile_reset": (_c.c_int, [_vp]),
+    "gol_set_tuning": (_c.c_int, [_vp, _c.c_int32, _c.c_int32]),
+    "gol_selftest": (_c.c_int, [_c.c_int, _u32p]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libgol.so not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _strerror(code: int) -> str:
+    return lib.gol_strerror(code).decode()
+
+
+def check(code: int, ctx=None) -> None:
+    if code != GOL_OK:
+        msg = lib.gol_last_error(ctx)
+        raise GolError(code, msg.decode() if msg else "")
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Names of the functions declared in include/gol.h."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(gol_\w+)\s*\(", text, re.M)))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(lib.gol_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def shard_rows(height: int, rank: int, nranks: int) -> tuple[int, int]:
+    r0, rows = ctypes.c_int64(0), ctypes.c_int64(0)
+    check(lib.gol_shard_rows(height, rank, nranks, ctypes.byref(r0), ctypes.byref(rows)))
+    return r0.value, rows.value
+
+
+def unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * GOL_UNIQUE_ID_BYTES)()
+    check(lib.gol_comm_unique_id(buf))
+    return bytes(buf)

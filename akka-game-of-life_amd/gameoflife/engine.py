@@ -1,0 +1,148 @@
+"""Shard engine: one libgol context = one backend worker owning a row block.
+
+The reference's backend hosts cell actors (CellActor.scala:10-102), each
+holding its own history and computing its next state by messaging its
+neighbours.  Here a backend worker owns a contiguous row block of the board in
+HBM and advances all of it per generation through libgol.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .rules import Rule, rule_by_name
+
+
+class GolEngine:
+    """A shard context on one GPU (gol_create .. gol_destroy)."""
+
+    def __init__(self, width: int, height: int, *, topology: str = "torus",
+                 rule: Rule | str = "life", device: int = 0, row0: int = 0,
+                 rows: int | None = None, vis: tuple[int, int] | None = None):
+        self.rule = rule_by_name(rule) if isinstance(rule, str) else rule
+        self.topology = topology
+        topo = {"torus": N.GOL_TORUS, "ref-clipped": N.GOL_REF_CLIPPED}[topology]
+        cfg = N.GolConfig()
+        cfg.width = width
+        cfg.height = height
+        cfg.row0 = row0
+        cfg.rows = (height - row0) if rows is None else rows
+        cfg.topology = topo
+        cfg.birth_mask = self.rule.birth
+        cfg.survive_mask = self.rule.survive
+        cfg.device = device
+        cfg.vis_width, cfg.vis_height = vis if vis is not None else (0, 0)
+        h = ctypes.c_void_p()
+        N.check(N.lib.gol_create(ctypes.byref(h), ctypes.byref(cfg)))
+        self._h = h
+        self.width, self.height = width, height
+        self.row0, self.rows = row0, cfg.rows
+        self.wwords = (width + 31) // 32
+        self.device = device
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            N.lib.gol_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int) -> None:
+        N.check(rc, self._h)
+
+    # -- state -------------------------------------------------------------
+    def seed(self, seed: int = 0x5EED) -> None:
+        self._chk(N.lib.gol_seed(self._h, seed))
+
+    def load(self, packed: np.ndarray) -> None:
+        a = np.ascontiguousarray(packed, dtype=np.uint32)
+        assert a.shape[0] == self.rows and a.shape[1] >= self.wwords, a.shape
+        self._chk(N.lib.gol_load(self._h, a.ctypes.data_as(N._u32p), a.shape[1]))
+
+    def snapshot(self) -> np.ndarray:
+        out = np.zeros((self.rows, self.wwords), dtype=np.uint32)
+        self._chk(N.lib.gol_snapshot(self._h, out.ctypes.data_as(N._u32p), self.wwords))
+        return out
+
+    def step(self, generations: int = 1, hashes: bool = False):
+        """Advance; returns the per-generation partial hashes (uint64) if asked."""
+        if hashes:
+            out = np.zeros(generations, dtype=np.uint64)
+            self._chk(N.lib.gol_step(self._h, generations, out.ctypes.data_as(N._u64p)))
+            return out
+        self._chk(N.lib.gol_step(self._h, generations, None))
+        return None
+
+    def sync(self) -> None:
+        self._chk(N.lib.gol_sync(self._h))
+
+    @property
+    def epoch(self) -> int:
+        e = ctypes.c_uint64(0)
+        self._chk(N.lib.gol_epoch(self._h, ctypes.byref(e)))
+        return e.value
+
+    def hash(self) -> int:
+        h = ctypes.c_uint64(0)
+        self._chk(N.lib.gol_hash(self._h, ctypes.byref(h)))
+        return h.value
+
+    def get_cell(self, x: int, y: int) -> bool:
+        s = ctypes.c_int(0)
+        self._chk(N.lib.gol_get_cell(self._h, x, y, ctypes.byref(s)))
+        return bool(s.value)
+
+    def checkpoint(self) -> bytes:
+        n = ctypes.c_size_t(0)
+        self._chk(N.lib.gol_checkpoint_bytes(self._h, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        self._chk(N.lib.gol_checkpoint(self._h, buf, n.value))
+        return buf.raw
+
+    def restore(self, blob: bytes) -> None:
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        self._chk(N.lib.gol_restore(self._h, buf, len(blob)))
+
+    # -- multi-GPU -----------------------------------------------------------
+    def comm_init(self, uid: bytes, rank: int, nranks: int) -> None:
+        arr = (ctypes.c_uint8 * N.GOL_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        self._chk(N.lib.gol_comm_init(self._h, arr, rank, nranks))
+
+    def allreduce_u64(self, values: np.ndarray) -> np.ndarray:
+        v = np.ascontiguousarray(values, dtype=np.uint64).copy()
+        self._chk(N.lib.gol_comm_allreduce_u64(self._h, v.ctypes.data_as(N._u64p), v.size))
+        return v
+
+    # -- timing / tuning -----------------------------------------------------
+    def profile(self, enable: bool = True) -> None:
+        self._chk(N.lib.gol_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_read(self) -> tuple[float, int]:
+        ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
+        self._chk(N.lib.gol_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def profile_reset(self) -> None:
+        self._chk(N.lib.gol_profile_reset(self._h))
+
+    def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0) -> None:
+        self._chk(N.lib.gol_set_tuning(self._h, band_rows, gens_per_pass))
+
+
+def selftest(device: int = 0) -> np.ndarray:
+    rep = np.zeros(256, dtype=np.uint32)
+    N.check(N.lib.gol_selftest(device, rep.ctypes.data_as(N._u32p)))
+    return rep

@@ -1,0 +1,186 @@
+#!/usr/bin/env python3
+"""bench.py -- generation-step throughput (GCUPS) + HBM roofline fraction.
+
+Workload (BASELINE.json configs[3], DESIGN.md "Measurement"): a 262144 x
+262144 torus, B3/S23, Bernoulli(0.5) splitmix64 board (seed 0x5EED),
+row-sharded over N GPUs (strong scaling; N = 1 runs the whole board on one
+GPU).  A "step" is one generation of the whole board.  At N = 1 the
+single-GPU roofline run of configs[2] (65536^2) is measured too and reported
+under "secondary".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+value = W*H*K / max-over-ranks wall time of the K timed generations (GCUPS),
+with the board already resident in HBM.  roofline.achieved = algorithmic bytes
+(0.25 B per cell-update: 1 bit read + 1 bit written) per step-kernel launch /
+the launch's average duration from HIP events on the launch stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_CELL_UPDATE = 0.25
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
+    ap.add_argument("--band", type=int, default=0, help="rows per band (0 = auto)")
+    ap.add_argument("--hash", action="store_true", help="fuse the per-generation state hash")
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def dist_setup(n):
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n:
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}")
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    return torch, dist, rank, world, local
+
+
+def barrier(dist, world):
+    if world > 1:
+        dist.barrier()
+
+
+def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
+    eng.step(warmup, hashes=with_hash)
+    eng.sync()
+    eng.profile(True)
+    eng.profile_reset()
+    barrier(dist, world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.step(steps, hashes=with_hash)
+    eng.sync()
+    torch.cuda.synchronize()
+    barrier(dist, world)
+    dt = time.perf_counter() - t0
+    kms, launches = eng.profile_read()
+    eng.profile(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, kms, launches
+
+
+def cpu_baseline(width, seconds):
+    """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
+    workload: a torus of the same width and 1024 rows, run for ~`seconds`."""
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    H = 1024
+    board = O.seed_packed(width, H, 0x5EED)
+    O.run_packed(board, width, 1, nthreads=threads, want_hashes=False)  # warm
+    gens, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        board, _ = O.run_packed(board, width, 4, nthreads=threads, want_hashes=False)
+        gens += 4
+    dt = time.perf_counter() - t0
+    return {"value": round(width * H * gens / dt / 1e9, 3), "unit": "GCUPS", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle_run_packed (oracle/gol_oracle.c), {width}x{H} torus B3/S23 slice of "
+                      f"the same workload, {gens} generations in {dt:.1f} s, {threads} OpenMP threads"}
+
+
+def main():
+    a = parse()
+    torch, dist, rank, world, local = dist_setup(a.gpus)
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+
+    W = H = a.board
+    row0, rows = N.shard_rows(H, rank, world)
+    eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
+    if a.band:
+        eng.set_tuning(band_rows=a.band)
+    if world > 1:
+        uid = N.unique_id() if rank == 0 else bytes(N.GOL_UNIQUE_ID_BYTES)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        eng.comm_init(bytes(t.tolist()), rank, world)
+    eng.seed(0x5EED)
+
+    dt, kms, launches = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    value = W * H * a.steps / dt / 1e9
+    # dominant kernel: the full-shard (N=1) or interior (N>1) step launch
+    cells_per_launch = W * (rows if world == 1 else max(rows - 2, 0))
+    avg_s = kms / 1e3 / max(launches, 1)
+    achieved = cells_per_launch * BYTES_PER_CELL_UPDATE / avg_s / 1e9 if launches else None
+    out = {
+        "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X + % of HBM roofline",
+        "value": round(value, 2),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(dt / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32 (bit-packed cells)",
+        "data": "synthetic (splitmix64 Bernoulli(0.5) board, seed 0x5EED)",
+        "config": {"workload": f"{W}x{H} torus B3/S23 row-sharded over {world} GPU(s) "
+                               f"(BASELINE.json configs[3]; N=1 = whole board on one GPU)",
+                   "board": [W, H], "rule": "B3/S23", "topology": "torus",
+                   "parallelism": f"row-block x{world}, RCCL halo send/recv",
+                   "fused_hash": bool(a.hash)},
+        "roofline": {"bound": "hbm",
+                     "achieved": round(achieved, 1) if achieved else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": None,
+                     "kernel": "gol::step_kernel<VEC=4,LIFE,...>",
+                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
+                     "algorithmic_bytes_per_launch": cells_per_launch * BYTES_PER_CELL_UPDATE},
+    }
+    eng.close()
+
+    if rank == 0 and world == 1:
+        if not a.no_secondary:
+            S = 65536
+            with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
+                e2.seed(0x5EED)
+                dt2, kms2, n2 = timed_run(e2, torch, dist, 1, max(a.steps, 20), a.warmup, a.hash)
+                avg2 = kms2 / 1e3 / max(n2, 1)
+                ach2 = S * S * BYTES_PER_CELL_UPDATE / avg2 / 1e9
+                out["secondary"] = {
+                    "workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
+                    "value": round(S * S * max(a.steps, 20) / dt2 / 1e9, 2), "unit": "GCUPS",
+                    "ms_per_step": round(dt2 / max(a.steps, 20) * 1e3, 4),
+                    "roofline": {"achieved": round(ach2, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(ach2 / HBM_PEAK_GBS, 4),
+                                 "avg_launch_ms": round(avg2 * 1e3, 4)}}
+        if not a.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

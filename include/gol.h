@@ -1,0 +1,186 @@
+/*
+ * gol.h -- C ABI of libgol, the MI355X-native generation-step engine.
+ *
+ * This is the drop-in boundary for the reference's hot path: the cell-actor
+ * generation step of almendar/akka-game-of-life.  The reference has no FFI;
+ * its "interface" is the Akka cell protocol.  Each entry point below names
+ * the reference interface it replaces (paths relative to
+ * src/main/scala/gameoflife/ of the reference).
+ *
+ * Conventions (DESIGN.md "Boundary"):
+ *   - Plain C types only: POD structs, pointers and sizes.  No torch types.
+ *   - Return 0 (GOL_OK) on success, a GOL_E* code otherwise; a per-context
+ *     message is available from gol_last_error().  A JVM/ctypes shim maps a
+ *     nonzero code to an exception, which is where the reference's supervisor
+ *     Restart (BoardCreator.scala:42-45) would take over.
+ *   - A context owns device memory on one GPU.  Host buffers belong to the
+ *     caller.  A context is not re-entrant, but calls may arrive from any OS
+ *     thread (actor dispatchers): every entry point re-binds its device.
+ *   - There is no CPU fallback: a context can only be created on a HIP
+ *     device; without one gol_create() fails with GOL_ENODEV.
+ *
+ * Board layout in HBM: bit-packed rows, row = y, bit (x % 32) of 32-bit word
+ * (x / 32) is cell x (LSB first); words per row = ceil(width / 32); bits at
+ * x >= width are zero.  Two device planes (current / next) are swapped after
+ * every generation.
+ */
+#ifndef GOL_H
+#define GOL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GOL_ABI_VERSION 1
+
+/* Return codes. */
+#define GOL_OK 0
+#define GOL_EINVAL 1   /* bad argument / unsupported geometry               */
+#define GOL_EHIP 2     /* HIP runtime error                                 */
+#define GOL_ENOMEM 3   /* device or host allocation failed                  */
+#define GOL_ECOMM 4    /* RCCL error / communicator not initialised         */
+#define GOL_ESTATE 5   /* call not valid in the context's current state     */
+#define GOL_ENODEV 6   /* no HIP device (no CPU fallback exists)            */
+
+/* Topologies. */
+#define GOL_TORUS 0        /* wrap in x and y (BASELINE.json configs 2-5)     */
+#define GOL_REF_CLIPPED 1  /* reference geometry: (w+1)x(h+1) cells, neighbours
+                              only from [0,w)x[0,h) (BoardCreator.scala:47-53,
+                              package.scala:17-28)                            */
+
+/* Life-like rules as (birth_mask, survive_mask): bit k set = the rule fires
+ * at k live neighbours.  NextStateCellGathererActor.scala:42-44. */
+#define GOL_RULE_LIFE_BIRTH 0x008u          /* B3/S23 (north_star)          */
+#define GOL_RULE_LIFE_SURVIVE 0x00Cu
+#define GOL_RULE_REF_LITERAL_BIRTH 0x000u   /* line 44 with a multiset count */
+#define GOL_RULE_REF_LITERAL_SURVIVE 0x1F7u
+#define GOL_RULE_REF_EFFECTIVE_BIRTH 0x000u /* line 42's Set collapse: the   */
+#define GOL_RULE_REF_EFFECTIVE_SURVIVE 0x1FFu /* identity, what actually runs */
+
+#define GOL_UNIQUE_ID_BYTES 128
+
+typedef struct gol_ctx gol_ctx;
+
+/* Board / shard description.  Replaces the BoardCreator constructor inputs
+ * (boardSize, BoardCreator.scala:18; application.conf:29-35) plus the cell
+ * placement (BoardCreator.scala:65-70): a context owns the row block
+ * [row0, row0 + rows) of a width x height board. */
+typedef struct gol_config {
+    int64_t width;          /* cells per row (torus: multiple of 32)          */
+    int64_t height;         /* rows of the global board                       */
+    int64_t row0;           /* first global row owned by this context         */
+    int64_t rows;           /* rows owned (0 => height - row0)                */
+    int32_t topology;       /* GOL_TORUS or GOL_REF_CLIPPED                   */
+    uint32_t birth_mask;    /* 9-bit masks, see GOL_RULE_*                    */
+    uint32_t survive_mask;
+    int32_t device;         /* HIP device ordinal                             */
+    int64_t vis_width;      /* REF_CLIPPED: visible columns (0 => width-1)    */
+    int64_t vis_height;     /* REF_CLIPPED: visible rows    (0 => height-1)   */
+} gol_config;
+
+/* Create a shard context.  Replaces createAllInitialActors
+ * (BoardCreator.scala:79-89) + CellActor construction (CellActor.scala:10,
+ * 34: epochToState = Map(0 -> initialState)).  The board starts all dead at
+ * epoch 0; fill it with gol_seed() or gol_load(). */
+int gol_create(gol_ctx** out, const gol_config* cfg);
+
+/* Free device memory and streams.  Replaces stopping the cell actors. */
+void gol_destroy(gol_ctx* ctx);
+
+/* Last error message of this context ("" if none); ctx may be NULL for the
+ * process-wide last error (e.g. a failed gol_create). */
+const char* gol_last_error(const gol_ctx* ctx);
+const char* gol_strerror(int code);
+int gol_abi_version(void);
+
+/* Number of HIP devices visible to this process (0 on a CPU-only host). */
+int gol_device_count(int* count);
+
+/* Row-block decomposition used for sharding (DESIGN.md "Multi-GPU"): rank r
+ * of n owns rows [row0, row0 + rows) of a board `height` rows tall.  Pure
+ * host arithmetic.  Replaces the random placement of BoardCreator.scala:33-36. */
+int gol_shard_rows(int64_t height, int rank, int nranks, int64_t* row0, int64_t* rows);
+
+/* Seed the shard with the counter-based splitmix64 board (Bernoulli(0.5)),
+ * identical for any sharding; resets the epoch to 0.  Seeded stand-in for
+ * BoardCreator.scala:23 (initialState = Random.nextBoolean() per cell). */
+int gol_seed(gol_ctx* ctx, uint64_t seed);
+
+/* Load the shard from host memory: `rows` x `host_pitch_words` packed words
+ * (row 0 = global row row0).  Resets the epoch to 0.  Replaces the per-cell
+ * initialState constructor argument (BoardCreator.scala:67-68). */
+int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words);
+
+/* Advance `generations` generations.  Replaces one NextStep tick
+ * (BoardCreator.scala:113-116) -> CurrentEpochMsg -> GetToNextEpoch ->
+ * NextStateCellGathererActor gather/count/rule -> SetNewStateMsg commit
+ * (CellActor.scala:63-91, NextStateCellGathererActor.scala:25-48), for every
+ * cell of the shard at once.  If hashes_out is not NULL it receives, for each
+ * generation, the shard's partial state hash (DESIGN.md "State hash"); the
+ * global hash is the sum mod 2^64 of the shards' partials.  With a
+ * communicator attached, halo rows are exchanged over RCCL every generation.
+ * Asynchronous when hashes_out is NULL (call gol_sync to wait). */
+int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out);
+
+/* Current epoch (CellActor.scala:39 myCurrentEpoch). */
+int gol_epoch(const gol_ctx* ctx, uint64_t* epoch);
+
+/* Block until all work queued on the context's streams is complete. */
+int gol_sync(gol_ctx* ctx);
+
+/* Partial state hash of the shard's current board. */
+int gol_hash(gol_ctx* ctx, uint64_t* hash_out);
+
+/* Copy the shard's current board to host: rows x host_pitch_words words.
+ * Replaces the CellStateMsg stream to the LoggerActor
+ * (CellActor.scala:89, LoggerActor.scala:30-46). */
+int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words);
+
+/* State of one cell of the shard at the current epoch (0/1).  Replaces the
+ * GetStateFromEpoch -> StateForEpoch exchange (CellActor.scala:71-77). */
+int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state);
+
+/* Shard checkpoint = {header with epoch + geometry, packed board}.  Replaces
+ * the reference's recovery state (initialState kept by the frontend,
+ * BoardCreator.scala:23,144, plus each cell's never-pruned history,
+ * CellActor.scala:34,81) used when a cell is re-deployed
+ * (BoardCreator.scala:138-154). */
+int gol_checkpoint_bytes(const gol_ctx* ctx, size_t* bytes);
+int gol_checkpoint(gol_ctx* ctx, void* host_out, size_t bytes);
+int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes);
+
+/* Multi-GPU: RCCL communicator over the ring of row-block shards.  Replaces
+ * the cross-backend neighbour messages (GetStateFromEpoch/StateForEpoch over
+ * Akka remote, application.conf:11-17).  Rank 0 calls gol_comm_unique_id and
+ * distributes the bytes; every rank then calls gol_comm_init. */
+int gol_comm_unique_id(uint8_t id_out[GOL_UNIQUE_ID_BYTES]);
+int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank, int nranks);
+
+/* Sum-reduce `count` uint64 values (mod 2^64) across the communicator in
+ * place (the per-generation hash reduction). */
+int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count);
+
+/* Kernel timing: when enabled, every step-kernel launch is bracketed by HIP
+ * events on the stream it runs on.  gol_profile_read returns the summed
+ * duration (ms) and the number of launches since the last reset. */
+int gol_profile_enable(gol_ctx* ctx, int enable);
+int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches);
+int gol_profile_reset(gol_ctx* ctx);
+
+/* Tuning knobs (0 = automatic): rows per band streamed by one wave, and the
+ * number of generations fused per pass (temporal blocking; 1 = none). */
+int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass);
+
+/* Diagnostic: runs a one-wave kernel exercising the cross-lane primitives the
+ * step kernel relies on (DPP wave shifts, v_alignbit, scalar loads) and
+ * writes 256 words to report (layout: gol_kernels.hip selftest_kernel). */
+int gol_selftest(int device, uint32_t* report);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GOL_H */

@@ -1,0 +1,45 @@
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "akka-game-of-life_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def _ensure_built():
+    """Build the oracle and libgol in-tree if they are missing (hipcc
+    cross-compiles gfx950 without a GPU)."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "liboracle.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True,
+                       stdout=subprocess.DEVNULL)
+    if not os.path.exists(os.path.join(PKG, "lib", "libgol.so")) and shutil.which("hipcc"):
+        subprocess.run(["make", "-C", PKG, "-j4"], check=True, stdout=subprocess.DEVNULL)
+
+
+_ensure_built()
+
+
+def _gpu_available() -> bool:
+    try:
+        from gameoflife import _native as N
+        return N.device_count() > 0
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    if not _gpu_available():
+        pytest.fail("no HIP device: -m gpu tests need an MI355X")
+    return 0

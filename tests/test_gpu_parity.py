@@ -1,0 +1,214 @@
+"""GPU parity: libgol (HIP, gfx950) vs the CPU oracle, through the C ABI.
+
+Bar: bit-exact boards and per-generation state hashes (integer/bit work).
+Oracle: oracle/ (parity unpinned -- see oracle/gol_oracle.c header).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+RULES = {"life": O.LIFE, "ref-literal": O.REF_LITERAL, "ref-effective": O.REF_EFFECTIVE}
+
+
+def engine(*a, **k):
+    from gameoflife.engine import GolEngine
+    return GolEngine(*a, **k)
+
+
+def rule_obj(rule):
+    from gameoflife.rules import Rule
+    return Rule(rule[0], rule[1])
+
+
+def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0):
+    topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
+    if cells is not None:
+        board = O.pack(cells)
+    else:
+        board = O.seed_packed(W, H, seed if seed is not None else 0x5EED)
+    with engine(W, H, topology=topology, rule=rule_obj(rule)) as e:
+        if band:
+            e.set_tuning(band_rows=band)
+        e.load(board)
+        assert e.hash() == O.hash_packed(board, W)
+        got = e.step(gens, hashes=True)
+        final_gpu = e.snapshot()
+        assert e.epoch == gens
+    final_cpu, want = O.run_packed(board, W, gens, topo, rule)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first hash mismatch at generation {bad[0] + 1} ({W}x{H} {topology} {rule})"
+    np.testing.assert_array_equal(final_gpu, final_cpu)
+
+
+def test_selftest_cross_lane(gpu):
+    from gameoflife.engine import selftest
+    rep = selftest(gpu)
+    inp = np.array([(0x01000193 * (i + 1) ^ (i << 24)) & 0xFFFFFFFF for i in range(64)],
+                   dtype=np.uint64).astype(np.uint32)
+    shr = np.concatenate([[0xA0A0A0A0], inp[:-1]]).astype(np.uint32)
+    shl = np.concatenate([inp[1:], [0xB0B0B0B0]]).astype(np.uint32)
+    np.testing.assert_array_equal(rep[0:64], shr)
+    np.testing.assert_array_equal(rep[64:128], shl)
+    prev = np.roll(inp, 1)
+    align = ((inp.astype(np.uint64) << 1) | (prev.astype(np.uint64) >> 31)) & 0xFFFFFFFF
+    np.testing.assert_array_equal(rep[128:192], align.astype(np.uint32))
+    assert (rep[192:256] == inp[5]).all()
+
+
+def test_seed_matches_oracle(gpu):
+    for W, H in [(4096, 64), (100, 7), (32 * 300, 33)]:
+        topo = "torus" if W % 32 == 0 else "ref-clipped"
+        with engine(W, H, topology=topo) as e:
+            e.seed(0x5EED)
+            np.testing.assert_array_equal(e.snapshot(), O.seed_packed(W, H, 0x5EED))
+            assert e.hash() == O.hash_packed(O.seed_packed(W, H, 0x5EED), W)
+
+
+# words per row covering VEC=1/2/4, partial strips, single word, many strips
+TORUS_SHAPES = [(32, 8), (64, 3), (96, 17), (32 * 63, 5), (32 * 64, 9), (32 * 128, 40),
+                (32 * 130, 11), (32 * 256, 33), (32 * 260, 7), (32 * 1024, 70), (32 * 2048, 4)]
+
+
+@pytest.mark.parametrize("W,H", TORUS_SHAPES)
+def test_torus_life(gpu, W, H):
+    check_run(W, H, 12, O.LIFE, "torus", seed=W * 7 + H)
+
+
+@pytest.mark.parametrize("H", [1, 2, 3])
+def test_torus_tiny_heights(gpu, H):
+    # rows alias on a torus shorter than 3 rows (multiset count)
+    check_run(32 * 8, H, 6, O.LIFE, "torus", seed=H)
+    check_run(32 * 8, H, 6, (0x1A4, 0x03B), "torus", seed=H)
+
+
+@pytest.mark.parametrize("band", [1, 2, 3, 5, 7, 16, 1000])
+def test_band_sizes(gpu, band):
+    # short bands exercise the boustrophedon direction switch and ring tails
+    check_run(32 * 256, 61, 5, O.LIFE, "torus", seed=band, band=band)
+    check_run(32 * 4, 23, 5, (0x049, 0x16E), "torus", seed=band, band=band)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_torus_random_rules(gpu, seed):
+    rng = np.random.default_rng(seed)
+    rule = (int(rng.integers(0, 512)), int(rng.integers(0, 512)))
+    W = 32 * int(rng.choice([1, 3, 64, 130, 256, 300]))
+    H = int(rng.integers(1, 50))
+    check_run(W, H, 8, rule, "torus", seed=seed)
+
+
+@pytest.mark.parametrize("name", list(RULES))
+def test_torus_named_rules(gpu, name):
+    check_run(32 * 96, 31, 10, RULES[name], "torus", seed=3)
+
+
+CLIPPED_SHAPES = [(7, 7), (2, 2), (33, 40), (100, 65), (32, 9), (1000, 37), (32 * 300 + 5, 12),
+                  (64 * 32 + 1, 20)]
+
+
+@pytest.mark.parametrize("W,H", CLIPPED_SHAPES)
+@pytest.mark.parametrize("name", list(RULES))
+def test_ref_clipped(gpu, W, H, name):
+    rng = np.random.default_rng(W * 31 + H)
+    cells = (rng.random((H, W)) < 0.45).astype(np.uint8)
+    check_run(W, H, 6, RULES[name], "ref-clipped", cells=cells)
+
+
+def test_ref_clipped_random_rules(gpu):
+    rng = np.random.default_rng(99)
+    for _ in range(6):
+        rule = (int(rng.integers(0, 512)), int(rng.integers(0, 512)))
+        W, H = int(rng.integers(2, 400)), int(rng.integers(2, 60))
+        cells = (rng.random((H, W)) < 0.5).astype(np.uint8)
+        check_run(W, H, 5, rule, "ref-clipped", cells=cells)
+
+
+def test_golden_ref_default_board(gpu):
+    """BASELINE.json config 1 geometry: the reference's default 6x6 board =
+    7x7 cells, java.util.Random-seeded, 100 generations, all three rules."""
+    for entry in GOLDEN["ref_default"]:
+        w, h = entry["w"], entry["h"]
+        cells = np.array([[int(ch) for ch in row] for row in entry["initial"]], dtype=np.uint8)
+        assert (cells == O.java_random_cells(w, h, entry["java_seed"])).all()
+        for name, res in entry["modes"].items():
+            with engine(w + 1, h + 1, topology="ref-clipped", rule=name) as e:
+                e.load(O.pack(cells))
+                got = e.step(100, hashes=True)
+                assert [int(x) for x in got] == res["hashes"], (entry["java_seed"], name)
+                final = O.unpack(e.snapshot(), w + 1)
+                want = np.array([[int(ch) for ch in row] for row in res["boards"][-1]["cells"]])
+                assert (final == want).all()
+
+
+def test_golden_torus_4096_1000(gpu):
+    """BASELINE.json config 2: 4096^2 torus B3/S23, 1000 generations,
+    per-generation hashes bit-exact against the committed oracle vectors."""
+    for g in GOLDEN["torus"]:
+        with engine(g["W"], g["H"], topology="torus", rule=g["rule"]) as e:
+            e.seed(g["seed"])
+            assert e.hash() == g["hash0"]
+            got = e.step(g["gens"], hashes=True)
+            bad = np.nonzero(got != np.array(g["hashes"], dtype=np.uint64))[0]
+            assert bad.size == 0, f"{g['W']}x{g['H']}: first mismatch at generation {bad[0] + 1}"
+            assert e.hash() == g["final_hash"]
+
+
+def test_fused_hash_equals_standalone_hash(gpu):
+    with engine(32 * 512, 300) as e:
+        e.seed(5)
+        for _ in range(4):
+            h = e.step(1, hashes=True)[0]
+            assert h == e.hash()
+
+
+def test_snapshot_get_cell_checkpoint(gpu):
+    W, H = 32 * 70, 50
+    with engine(W, H) as e:
+        e.seed(9)
+        e.step(7)
+        snap = e.snapshot()
+        cells = O.unpack(snap, W)
+        for (x, y) in [(0, 0), (W - 1, H - 1), (123, 17), (31, 32), (32, 1)]:
+            assert e.get_cell(x, y) == bool(cells[y, x])
+        blob = e.checkpoint()
+        ref = e.step(5, hashes=True)
+        e.restore(blob)
+        assert e.epoch == 7
+        np.testing.assert_array_equal(e.snapshot(), snap)
+        np.testing.assert_array_equal(e.step(5, hashes=True), ref)
+
+
+def test_full_size_65536_bit_exact(gpu):
+    """BASELINE.json config 3 geometry (65536^2 torus): 3 generations checked
+    word-for-word against the multithreaded CPU oracle."""
+    W = H = 65536
+    with engine(W, H) as e:
+        e.seed(0x5EED)
+        got = e.step(3, hashes=True)
+        final = e.snapshot()
+    board = O.seed_packed(W, H, 0x5EED)
+    final_cpu, want = O.run_packed(board, W, 3, O.TORUS, O.LIFE)
+    np.testing.assert_array_equal(got, want)
+    assert (final == final_cpu).all()
+
+
+def test_known_patterns_on_gpu(gpu):
+    # glider on a 64x64 torus returns to its start after 4*64 generations
+    W = H = 64
+    cells = np.zeros((H, W), dtype=np.uint8)
+    for x, y in [(1, 0), (2, 1), (0, 2), (1, 2), (2, 2)]:
+        cells[y, x] = 1
+    with engine(W, H) as e:
+        e.load(O.pack(cells))
+        e.step(4)
+        shifted = np.roll(np.roll(cells, 1, 0), 1, 1)
+        assert (O.unpack(e.snapshot(), W) == shifted).all()
+        e.step(4 * 64 - 4)
+        assert (O.unpack(e.snapshot(), W) == cells).all()
