@@ -61,13 +61,14 @@ struct gol_ctx {
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
     // tuning
-    int32_t band_rows = 0, gens_per_pass = 1;
+    int32_t band_rows = 0, gens_per_pass = 1;  // gens_per_pass: temporal blocking depth
     // profiling
     bool prof = false;
     std::vector<EventPair> evs;
     size_t evs_used = 0;
     double prof_ms = 0.0;
     uint64_t prof_launches = 0;
+    uint64_t prof_gens = 0;  // generations covered by the profiled launches
     std::string err;
 };
 
@@ -174,17 +175,20 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips) {
     return (int)band;
 }
 
-// Launch the step kernel over local row ranges [lo0,hi0) (+ [lo1,hi1) if n==2).
-// Only the main launch of a generation (whole shard, or the interior rows of
-// a sharded shard) is bracketed by profiling events: it is the dominant kernel.
-int launch_ranges(gol_ctx* ctx, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
-                  const uint32_t* hbot, unsigned long long* slots, int n, const int32_t* lo,
-                  const int32_t* hi, bool main_launch) {
+// Launch one pass of `gens` generations over local row ranges [lo0,hi0)
+// (+ [lo1,hi1) if n == 2).  Only the main launch of a pass (whole shard, or
+// the interior rows of a sharded shard) is bracketed by profiling events: it
+// is the dominant kernel.
+int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
+                  const uint32_t* hbot, int64_t halo_stride, bool wrap_y, unsigned long long* slots, int n,
+                  const int32_t* lo, const int32_t* hi, bool main_launch) {
     gol::StepParams p{};
     p.cur = cur;
     p.nxt = nxt;
     p.halo_top = htop;
     p.halo_bot = hbot;
+    p.halo_stride = halo_stride;
+    p.wrap_y = wrap_y ? 1 : 0;
     p.hash_slots = slots;
     p.pitch = ctx->pitch;
     p.grow0 = ctx->row0;
@@ -193,7 +197,8 @@ int launch_ranges(gol_ctx* ctx, const uint32_t* cur, uint32_t* nxt, const uint32
     p.width = ctx->width;
     p.wwords = ctx->wwords;
     p.rows = (int32_t)ctx->rows;
-    p.strips = (int32_t)((ctx->wwords + gol::kWaveLanes * ctx->vec - 1) / (gol::kWaveLanes * ctx->vec));
+    const int sw = gol::strip_words(ctx->vec, gens);
+    p.strips = (int32_t)((ctx->wwords + sw - 1) / sw);
     int64_t maxlen = 0;
     for (int k = 0; k < n; ++k) maxlen = std::max<int64_t>(maxlen, hi[k] - lo[k]);
     p.band = pick_band(ctx, maxlen, p.strips);
@@ -222,65 +227,79 @@ int launch_ranges(gol_ctx* ctx, const uint32_t* cur, uint32_t* nxt, const uint32
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, ctx->vec, life, slots != nullptr, clipped, gx, n, ctx->compute));
-    if (ev) HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
+    HIP_CHECK(ctx, gol::launch_step(p, ctx->vec, gens, life, slots != nullptr, clipped, gx, n, ctx->compute));
+    if (ev) {
+        HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
+        ctx->prof_gens += (uint64_t)gens;
+    }
     return GOL_OK;
 }
 
-// One generation.  slots: this generation's hash accumulators or null.
-int one_generation(gol_ctx* ctx, unsigned long long* slots) {
+// One pass of G generations (temporal blocking, G <= kMaxGensPerPass).
+// slots: the hash accumulators of these G generations (G * kHashGenStride), or null.
+int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
     uint32_t* cur = ctx->plane[ctx->cur];
     uint32_t* nxt = ctx->plane[ctx->cur ^ 1];
     const int32_t rows = (int32_t)ctx->rows;
     const bool torus = ctx->topology == GOL_TORUS;
+    const int64_t pitch = ctx->pitch;
     if (!sharded(ctx)) {
-        const uint32_t* htop = torus ? cur + (int64_t)(rows - 1) * ctx->pitch : ctx->zero_row;
-        const uint32_t* hbot = torus ? cur : ctx->zero_row;
+        // torus: rows wrap inside the plane; clipped: outside rows are dead
         const int32_t lo[1] = {0}, hi[1] = {rows};
-        int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+        int rc = launch_ranges(ctx, G, cur, nxt, ctx->zero_row, ctx->zero_row, 0, torus, slots, 1, lo, hi, true);
         if (rc) return rc;
     } else {
         const int up = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
         const int down = (ctx->rank + 1) % ctx->nranks;
         const bool has_up = torus || ctx->rank > 0;
         const bool has_down = torus || ctx->rank < ctx->nranks - 1;
-        // Halo exchange on the comm stream once the current plane is final.
+        // G-deep halo exchange on the comm stream once the current plane is final.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
+        const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
         NCCL_CHECK(ctx, ncclGroupStart());
         // Issue order matters when up == down (2 ranks): per-peer FIFO matching
-        // pairs my last row with the peer's top halo and my first row with its
-        // bottom halo.
+        // pairs my last rows with the peer's top halo and my first rows with
+        // its bottom halo (gameoflife/shard.py HaloPlan mirrors this order).
         if (has_down)
-            NCCL_CHECK(ctx, ncclSend(cur + (int64_t)(rows - 1) * ctx->pitch, ctx->wwords, ncclUint32, down,
-                                     ctx->nccl, ctx->comm));
-        if (has_up) NCCL_CHECK(ctx, ncclSend(cur, ctx->wwords, ncclUint32, up, ctx->nccl, ctx->comm));
-        if (has_up) NCCL_CHECK(ctx, ncclRecv(ctx->halo_top, ctx->wwords, ncclUint32, up, ctx->nccl, ctx->comm));
-        if (has_down)
-            NCCL_CHECK(ctx, ncclRecv(ctx->halo_bot, ctx->wwords, ncclUint32, down, ctx->nccl, ctx->comm));
+            NCCL_CHECK(ctx, ncclSend(cur + (int64_t)(rows - G) * pitch, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
+        if (has_up) NCCL_CHECK(ctx, ncclSend(cur, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
+        if (has_up) NCCL_CHECK(ctx, ncclRecv(ctx->halo_top, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
+        if (has_down) NCCL_CHECK(ctx, ncclRecv(ctx->halo_bot, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
         NCCL_CHECK(ctx, ncclGroupEnd());
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
+        // A missing neighbour (clipped board ends) reads dead rows: zero_row
+        // holds kMaxGensPerPass of them at the same pitch as the halos.
         const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
         const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
-        if (rows > 2) {
-            // interior rows overlap the exchange; boundary rows follow it
-            const int32_t lo[1] = {1}, hi[1] = {rows - 1};
-            int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+        if (rows > 2 * G) {
+            // interior rows overlap the exchange; boundary row blocks follow it
+            const int32_t lo[1] = {G}, hi[1] = {rows - G};
+            int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
             if (rc) return rc;
             HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
-            const int32_t blo[2] = {0, rows - 1}, bhi[2] = {1, rows};
-            rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 2, blo, bhi, false);
+            const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
+            rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false);
             if (rc) return rc;
         } else {
             HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
             const int32_t lo[1] = {0}, hi[1] = {rows};
-            int rc = launch_ranges(ctx, cur, nxt, htop, hbot, slots, 1, lo, hi, true);
+            int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
             if (rc) return rc;
         }
     }
     ctx->cur ^= 1;
-    ctx->epoch += 1;
+    ctx->epoch += (uint64_t)G;
     return GOL_OK;
+}
+
+// Pass depth for the next `remaining` generations.
+int pass_depth(const gol_ctx* ctx, uint32_t remaining) {
+    int G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : 1;
+    G = std::min<int>(G, gol::kMaxGensPerPass);
+    G = std::min<int64_t>(G, remaining);
+    if (sharded(ctx)) G = std::min<int64_t>(G, ctx->rows);  // halo rows are sent from the shard
+    return std::max(G, 1);
 }
 
 void destroy_impl(gol_ctx* c) {
@@ -418,7 +437,8 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
             return fail(GOL_EHIP);
         }
     }
-    const size_t row_bytes = (size_t)ctx->pitch * sizeof(uint32_t);
+    // G-deep halos (receive buffers) and kMaxGensPerPass dead rows
+    const size_t row_bytes = (size_t)gol::kMaxGensPerPass * ctx->pitch * sizeof(uint32_t);
     if (hipMalloc(&ctx->halo_top, row_bytes) != hipSuccess || hipMalloc(&ctx->halo_bot, row_bytes) != hipSuccess ||
         hipMalloc(&ctx->zero_row, row_bytes) != hipSuccess) {
         set_err(ctx, GOL_ENOMEM, "halo allocation failed");
@@ -481,18 +501,24 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
     if (int rc = bind(ctx)) return rc;
     if (generations == 0) return GOL_OK;
     if (!hashes_out) {
-        for (uint32_t g = 0; g < generations; ++g)
-            if (int rc = one_generation(ctx, nullptr)) return rc;
+        for (uint32_t g = 0; g < generations;) {
+            const int G = pass_depth(ctx, generations - g);
+            if (int rc = one_pass(ctx, G, nullptr)) return rc;
+            g += (uint32_t)G;
+        }
         return GOL_OK;
     }
     constexpr uint32_t kChunk = 1024;
     for (uint32_t g0 = 0; g0 < generations; g0 += kChunk) {
         const uint32_t n = std::min(kChunk, generations - g0);
         if (int rc = ensure_slots(ctx, n)) return rc;
-        const size_t per = (size_t)gol::kHashSlots * gol::kHashSlotStride;
+        const size_t per = (size_t)gol::kHashGenStride;
         HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, n * per * sizeof(unsigned long long), ctx->compute));
-        for (uint32_t g = 0; g < n; ++g)
-            if (int rc = one_generation(ctx, ctx->slots + g * per)) return rc;
+        for (uint32_t g = 0; g < n;) {
+            const int G = pass_depth(ctx, n - g);
+            if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
+            g += (uint32_t)G;
+        }
         HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, n * per * sizeof(unsigned long long),
                                       hipMemcpyDeviceToHost, ctx->compute));
         HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
@@ -632,12 +658,13 @@ int gol_profile_enable(gol_ctx* ctx, int enable) {
     return GOL_OK;
 }
 
-int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches) {
+int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* generations) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (int rc = bind(ctx)) return rc;
     if (int rc = fold_profile(ctx)) return rc;
     if (total_ms) *total_ms = ctx->prof_ms;
     if (launches) *launches = ctx->prof_launches;
+    if (generations) *generations = ctx->prof_gens;
     return GOL_OK;
 }
 
@@ -647,15 +674,17 @@ int gol_profile_reset(gol_ctx* ctx) {
     if (int rc = fold_profile(ctx)) return rc;
     ctx->prof_ms = 0.0;
     ctx->prof_launches = 0;
+    ctx->prof_gens = 0;
     return GOL_OK;
 }
 
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
-    if (band_rows < 0 || gens_per_pass < 0) return set_err(ctx, GOL_EINVAL, "negative tuning value");
+    if (band_rows < 0 || gens_per_pass < 0 || gens_per_pass > gol::kMaxGensPerPass)
+        return set_err(ctx, GOL_EINVAL, "tuning out of range (band_rows >= 0, 0 <= gens_per_pass <= %d)",
+                       gol::kMaxGensPerPass);
     ctx->band_rows = band_rows;
-    ctx->gens_per_pass = gens_per_pass > 0 ? gens_per_pass : 1;
-    if (ctx->gens_per_pass != 1) return set_err(ctx, GOL_EINVAL, "gens_per_pass > 1 not available yet");
+    if (gens_per_pass > 0) ctx->gens_per_pass = gens_per_pass;
     return GOL_OK;
 }
 

@@ -10,20 +10,22 @@ constexpr int kWaveLanes = 64;   // CDNA wavefront
 constexpr int kWavesPerWG = 4;   // 256-thread workgroups
 constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line each)
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
+constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
+constexpr int kMaxGensPerPass = 4;  // temporal blocking depth supported by the kernels
 
 // Hash constants (DESIGN.md "State hash"; oracle/gol_oracle.c oracle_hash_packed).
 constexpr uint32_t kHashK1 = 0x9E3779B9u;
 constexpr uint32_t kHashK2 = 0x85EBCA6Bu;
 
-// One step launch over up to two local row ranges (blockIdx.y selects one):
-// the whole shard (single launch), or the interior / the two boundary rows
-// of a sharded generation.
+// One launch advances G generations (G = `gens`, 1..kMaxGensPerPass) over up
+// to two local row ranges (blockIdx.y selects one): the whole shard, or the
+// interior / the two boundary row blocks of a sharded pass.
 struct StepParams {
     const uint32_t* cur;       // local row 0 of the current plane
     uint32_t* nxt;             // local row 0 of the next plane
-    const uint32_t* halo_top;  // the row above local row 0
-    const uint32_t* halo_bot;  // the row below local row rows-1
-    unsigned long long* hash_slots;  // kHashSlots * kHashSlotStride u64, or null
+    const uint32_t* halo_top;  // rows -G .. -1 (halo_stride apart)
+    const uint32_t* halo_bot;  // rows rows .. rows+G-1
+    unsigned long long* hash_slots;  // G * kHashGenStride u64, or null
     int64_t pitch;             // words between rows (multiple of 64)
     int64_t grow0;             // global row of local row 0
     int64_t vis_rows;          // global rows [0, vis_rows) are visible (clipped)
@@ -34,16 +36,22 @@ struct StepParams {
     int32_t row_lo[2];
     int32_t row_hi[2];
     int32_t nbands[2];
-    int32_t band;              // rows streamed by one wave
-    int32_t strips;            // column strips per row = ceil(wwords / (64*VEC))
+    int32_t band;              // output rows streamed by one wave
+    int32_t strips;            // column strips per row
     int32_t wrap_x;            // torus in x
+    int32_t wrap_y;            // unsharded torus: local rows wrap modulo `rows`
+    int64_t halo_stride;       // words between halo rows (0: one row repeated)
     uint32_t birth;
     uint32_t survive;
 };
 
-// vec: words per lane (1, 2 or 4); life: B3/S23 fast path (torus only);
-// hash: fuse the state hash of the output; clipped: reference geometry.
-hipError_t launch_step(const StepParams& p, int vec, bool life, bool hash, bool clipped,
+// Strip geometry of a launch: words covered per wave.
+int strip_words(int vec, int gens);
+
+// vec: words per lane (1, 2 or 4); gens: generations per pass; life: B3/S23
+// fast path (torus only); hash: fuse the per-generation state hash; clipped:
+// reference geometry.
+hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped,
                        int grid_x, int grid_y, hipStream_t stream);
 
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width,

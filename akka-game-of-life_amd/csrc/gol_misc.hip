@@ -1,0 +1,100 @@
+// gol_misc.hip -- board seeding, standalone state hash, the cross-lane self
+// test, and the launch dispatcher over pass depths.
+#include <algorithm>
+
+#include "gol_stencil.h"
+
+namespace gol {
+
+namespace {
+
+typedef const __attribute__((address_space(4))) uint32_t* const_u32_ptr;
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// oracle/gol_oracle.c oracle_seed_packed, on device: the seeded stand-in for
+// BoardCreator.scala:23 (Random.nextBoolean() per cell).
+__global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0,
+                            int32_t rows, uint64_t seed) {
+    const int64_t total = (int64_t)rows * wwords;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = k / wwords, c = k % wwords;
+        const uint64_t i = (uint64_t)(grow0 + r) * (uint64_t)wwords + (uint64_t)c;
+        const uint64_t z = splitmix64(seed + 0x9E3779B97F4A7C15ull * (i + 1));
+        plane[r * pitch + c] = (uint32_t)(z >> 32) & dev::col_mask(width, c);
+    }
+}
+
+__global__ void hash_kernel(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0, int32_t rows,
+                            unsigned long long* slots) {
+    const int64_t total = (int64_t)rows * wwords;
+    unsigned long long acc = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = k / wwords, c = k % wwords;
+        const uint32_t g = (uint32_t)((uint64_t)(grow0 + r) * (uint64_t)wwords + (uint64_t)c);
+        acc += (unsigned long long)(plane[r * pitch + c] ^ (g * kHashK1)) *
+               (unsigned long long)((g * kHashK2) | 1u);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWaveLanes);
+    if ((threadIdx.x & (kWaveLanes - 1)) == 0)
+        atomicAdd(slots + (size_t)(blockIdx.x % kHashSlots) * kHashSlotStride, acc);
+}
+
+// out[0..63]    = dpp wave_shr:1 (old = 0xA0A0A0A0) of in[lane]
+// out[64..127]  = dpp wave_shl:1 (old = 0xB0B0B0B0) of in[lane]
+// out[128..191] = alignbit(in[lane], in[(lane+63)%64], 31)
+// out[192..255] = in[5] via a wave-uniform scalar load
+__global__ void selftest_kernel(const uint32_t* in, uint32_t* out) {
+    const int lane = threadIdx.x;
+    const uint32_t v = in[lane];
+    out[lane] = dev::dpp_shr1(0xA0A0A0A0u, v);
+    out[64 + lane] = dev::dpp_shl1(0xB0B0B0B0u, v);
+    out[128 + lane] = __builtin_amdgcn_alignbit(v, in[(lane + 63) % 64], 31);
+    out[192 + lane] = ((const_u32_ptr)in)[5];
+}
+
+}  // namespace
+
+int strip_words(int vec, int gens) { return (gens == 1 ? kWaveLanes : kWaveLanes - 2) * vec; }
+
+hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, int grid_x,
+                       int grid_y, hipStream_t stream) {
+    switch (gens) {
+        case 1: return launch_step_g1(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 2: return launch_step_g2(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 3: return launch_step_g3(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 4: return launch_step_g4(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0, int32_t rows,
+                       uint64_t seed, hipStream_t stream) {
+    const int64_t total = (int64_t)rows * wwords;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
+    hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(256), 0, stream, plane, pitch, wwords, width, grow0, rows,
+                       seed);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0, int32_t rows,
+                       unsigned long long* slots, hipStream_t stream) {
+    const int64_t total = (int64_t)rows * wwords;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
+    hipLaunchKernelGGL(hash_kernel, dim3(blocks), dim3(256), 0, stream, plane, pitch, wwords, grow0, rows, slots);
+    return hipGetLastError();
+}
+
+hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream) {
+    hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 0, stream, in, out);
+    return hipGetLastError();
+}
+
+}  // namespace gol

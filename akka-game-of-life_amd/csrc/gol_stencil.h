@@ -1,0 +1,525 @@
+// gol_stencil.h -- gfx950 (CDNA4) device code of the Life-like generation step.
+//
+// Replaces the reference's per-cell actor computation:
+//   NextStateCellGathererActor.scala:32-36  ask <=8 neighbours GetStateFromEpoch
+//   NextStateCellGathererActor.scala:39-46  gather, count, apply rule, commit e+1
+//   package.scala:17-28                     the clipped Moore neighbourhood
+// with one streaming stencil over a bit-packed board (DESIGN.md "Kernels").
+//
+// Work decomposition: each wave64 owns one column strip of one band of `band`
+// output rows and streams down (or up: odd bands run bottom-up, so both
+// neighbours of a band seam read it at the same time and the second read hits
+// the Infinity Cache) keeping a ring of rows in registers.  Every input word
+// is read from HBM once per pass and every output word written once.
+//
+// Neighbour count: vertical full adder (a + c + b) per column -> two bit
+// planes, DPP wave_shr:1 / wave_shl:1 bring the neighbouring lane's column
+// sums, v_alignbit funnel-shifts them to the x-1 / x+1 columns, and a
+// bit-sliced adder gives the 3x3 box sum T9 (4 bit planes).  B3/S23 is
+// "T9 == 3 | (alive & T9 == 4)"; the generic (birth, survive) path subtracts
+// the centre and evaluates the masks with a v_bfi mux tree.
+//
+// Two kernels:
+//   step_kernel      one generation per pass.  A strip is 64 lanes x VEC
+//                    words; the bits beyond the strip's edges come from one
+//                    extra dword load per row (lane 0: the word left of the
+//                    strip, other lanes: the word right of it) that DPP's
+//                    `old` operand hands to exactly the lanes without a
+//                    source lane.
+//   multistep_kernel G = 2..4 generations per pass (temporal blocking: HBM
+//                    traffic per generation / G).  Lanes 0 and 63 are halo
+//                    lanes holding the neighbouring strips' words; garbage
+//                    enters their outermost bit and moves one bit per
+//                    generation, far from the 32*VEC-bit lane edge, so the
+//                    62 inner lanes are exact.  The intermediate generations
+//                    live only in registers (one 3-row ring per stage) and
+//                    are hashed there; G-row halos come from above/below.
+#pragma once
+#include "gol_kernels.h"
+
+namespace gol {
+namespace dev {
+
+constexpr int kPF = 2;               // step_kernel: rows prefetched ahead
+constexpr int kRing = kPF + 3;       // step_kernel: register ring of stream rows
+constexpr int kMPF = 3;              // multistep_kernel: rows prefetched ahead
+constexpr int kMRing = 6;            // multistep_kernel: input ring (multiple of 3)
+constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
+constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
+
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    return (m & a) | (~m & b);
+}
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kDppWaveShr1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl1(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kDppWaveShl1, 0xf, 0xf, false);
+}
+
+// Bits [0, limit) of word `w` set (limit in cells).
+__device__ __forceinline__ uint32_t col_mask(int64_t limit, int64_t w) {
+    const int64_t lo = w * 32;
+    if (lo + 32 <= limit) return 0xFFFFFFFFu;
+    if (lo >= limit) return 0u;
+    return (uint32_t)((1ull << (limit - lo)) - 1ull);
+}
+
+template <int VEC>
+struct Words {
+    uint32_t w[VEC];
+};
+
+// Unconditional load (callers clamp the column into the row), so no
+// exec-masked branch separates a load from its use and the compiler's
+// counted vmcnt waits keep the prefetch ring in flight.
+template <int VEC>
+__device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VEC>& d) {
+    if constexpr (VEC == 4) {
+        const uint4 v = *reinterpret_cast<const uint4*>(rp + col);
+        d.w[0] = v.x; d.w[1] = v.y; d.w[2] = v.z; d.w[3] = v.w;
+    } else if constexpr (VEC == 2) {
+        const uint2 v = *reinterpret_cast<const uint2*>(rp + col);
+        d.w[0] = v.x; d.w[1] = v.y;
+    } else {
+        d.w[0] = rp[col];
+    }
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_words(uint32_t* rp, int col, bool active, const Words<VEC>& d) {
+    if (active) {
+        if constexpr (VEC == 4) {
+            *reinterpret_cast<uint4*>(rp + col) = make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]);
+        } else if constexpr (VEC == 2) {
+            *reinterpret_cast<uint2*>(rp + col) = make_uint2(d.w[0], d.w[1]);
+        } else {
+            rp[col] = d.w[0];
+        }
+    }
+}
+
+// Local row pointer for r in [-G, rows + G).
+__device__ __forceinline__ const uint32_t* row_ptr(const StepParams& p, int r, int G) {
+    if (p.wrap_y) {
+        while (r < 0) r += p.rows;
+        while (r >= p.rows) r -= p.rows;
+        return p.cur + (int64_t)r * p.pitch;
+    }
+    if (r < 0) return p.halo_top + (int64_t)(r + G) * p.halo_stride;
+    if (r >= p.rows) return p.halo_bot + (int64_t)(r - p.rows) * p.halo_stride;
+    return p.cur + (int64_t)r * p.pitch;
+}
+
+template <bool CLIPPED>
+__device__ __forceinline__ bool row_visible(const StepParams& p, int r) {
+    if constexpr (CLIPPED) {
+        const int64_t g = p.grow0 + r;
+        return g >= 0 && g < p.vis_rows;
+    } else {
+        return true;
+    }
+}
+
+// Vertical 3-sums (v1 v0) = a + c + b of the visible rows.
+template <int VEC, bool CLIPPED>
+__device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC>& C, const Words<VEC>& B,
+                                            bool va, bool vc, bool vb, const uint32_t (&cmask)[VEC],
+                                            uint32_t (&v0)[VEC], uint32_t (&v1)[VEC], uint32_t (&cv)[VEC]) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        uint32_t a = A.w[j], c = C.w[j], b = B.w[j];
+        if constexpr (CLIPPED) {
+            a = va ? (a & cmask[j]) : 0u;
+            c = vc ? (c & cmask[j]) : 0u;
+            b = vb ? (b & cmask[j]) : 0u;
+        }
+        const uint32_t t = a ^ c;
+        v0[j] = t ^ b;
+        v1[j] = bfi(t, b, a);
+        cv[j] = c;
+    }
+}
+
+// The rule on one lane's VEC words given the column sums of its words and of
+// the words left (m0 m1) and right (n0 n1) of them.
+template <int VEC, bool LIFE>
+__device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (&v0)[VEC],
+                                           const uint32_t (&v1)[VEC], uint32_t m0, uint32_t m1,
+                                           uint32_t n0, uint32_t n1, const Words<VEC>& alive,
+                                           const uint32_t (&cv)[VEC], Words<VEC>& out) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t p0 = j == 0 ? m0 : v0[j - 1];
+        const uint32_t p1 = j == 0 ? m1 : v1[j - 1];
+        const uint32_t q0 = j == VEC - 1 ? n0 : v0[j + 1];
+        const uint32_t q1 = j == VEC - 1 ? n1 : v1[j + 1];
+        const uint32_t w0 = __builtin_amdgcn_alignbit(v0[j], p0, 31);  // column x-1
+        const uint32_t e0 = __builtin_amdgcn_alignbit(q0, v0[j], 1);   // column x+1
+        const uint32_t w1 = __builtin_amdgcn_alignbit(v1[j], p1, 31);
+        const uint32_t e1 = __builtin_amdgcn_alignbit(q1, v1[j], 1);
+        // T9 = (w1 w0) + (v1 v0) + (e1 e0) = s3 s2 s1 s0
+        const uint32_t t0 = w0 ^ v0[j];
+        const uint32_t s0 = t0 ^ e0;
+        const uint32_t c0 = bfi(t0, e0, w0);
+        const uint32_t t1 = w1 ^ v1[j];
+        const uint32_t pp = t1 ^ e1;
+        const uint32_t qq = bfi(t1, e1, w1);
+        const uint32_t s1 = pp ^ c0;
+        const uint32_t r2 = pp & c0;
+        const uint32_t s2 = qq ^ r2;
+        const uint32_t al = alive.w[j];
+        if constexpr (LIFE) {
+            // T9 mod 8 == 3, or alive and T9 mod 8 == 4 (T9 in {8,9} maps to {0,1}).
+            out.w[j] = bfi(s2, al & ~(s1 | s0), s1 & s0);
+        } else {
+            const uint32_t s3 = qq & r2;
+            // n = T9 - visible centre (a 1-bit borrow chain).
+            const uint32_t c = cv[j];
+            const uint32_t n0b = s0 ^ c, b0 = c & ~s0;
+            const uint32_t n1b = s1 ^ b0, b1 = b0 & ~s1;
+            const uint32_t n2b = s2 ^ b1, b2 = b1 & ~s2;
+            const uint32_t n3b = s3 ^ b2;
+            uint32_t L[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const uint32_t sm = ((p.survive >> k) & 1u) ? 0xFFFFFFFFu : 0u;
+                const uint32_t bm = ((p.birth >> k) & 1u) ? 0xFFFFFFFFu : 0u;
+                L[k] = bfi(al, sm, bm);
+            }
+            const uint32_t m01 = bfi(n0b, L[1], L[0]), m23 = bfi(n0b, L[3], L[2]);
+            const uint32_t m45 = bfi(n0b, L[5], L[4]), m67 = bfi(n0b, L[7], L[6]);
+            const uint32_t m03 = bfi(n1b, m23, m01), m47 = bfi(n1b, m67, m45);
+            const uint32_t m07 = bfi(n2b, m47, m03);
+            out.w[j] = bfi(n3b, L[8], m07);
+        }
+    }
+}
+
+// Hash term accumulation for one output row (DESIGN.md "State hash").
+template <int VEC>
+__device__ __forceinline__ void hash_row(const StepParams& p, int r, const uint32_t (&lk1)[VEC],
+                                         const uint32_t (&lk2)[VEC], const Words<VEC>& o,
+                                         unsigned long long& acc) {
+    const uint32_t gb = (uint32_t)((uint64_t)(p.grow0 + r) * (uint64_t)p.wwords);
+    const uint32_t rb1 = gb * kHashK1, rb2 = gb * kHashK2;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t k1 = rb1 + lk1[j];
+        const uint32_t k2 = (rb2 + lk2[j]) | 1u;
+        acc += (unsigned long long)(o.w[j] ^ k1) * (unsigned long long)k2;
+    }
+}
+
+// wave reduce -> workgroup reduce -> one atomic per workgroup into a sharded slot
+__device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long long* slots, int lane,
+                                           int wave_in_wg) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWaveLanes);
+    __shared__ unsigned long long part[kWavesPerWG];
+    __syncthreads();
+    if (lane == 0) part[wave_in_wg] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerWG; ++w) t += part[w];
+        atomicAdd(slots + (size_t)((blockIdx.x + blockIdx.y) % kHashSlots) * kHashSlotStride, t);
+    }
+}
+
+// --------------------------------------------------------------------------
+// One generation per pass.
+// --------------------------------------------------------------------------
+template <int VEC, bool LIFE, bool HASH, bool CLIPPED>
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
+    const int lane = threadIdx.x & (kWaveLanes - 1);
+    const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
+    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
+    const int rg = blockIdx.y;
+    const int strip = wave % p.strips;
+    const int bandi = wave / p.strips;
+    unsigned long long acc = 0;
+
+    if (bandi < p.nbands[rg]) {
+        const int r_begin = p.row_lo[rg] + bandi * p.band;
+        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int nrows = r_end - r_begin;
+        const int s0 = strip * (kWaveLanes * VEC);
+        const int nact = min(kWaveLanes, (p.wwords - s0) / VEC);
+        const int col = s0 + lane * VEC;
+        const bool active = lane < nact;
+        const int lcolumn = active ? col : s0;  // clamped load column
+        // Edge words; an edge outside a clipped board is read from a clamped
+        // in-row index and masked to zero.
+        int lcol = s0 - 1;
+        bool lvalid = true;
+        if (lcol < 0) { lvalid = p.wrap_x != 0; lcol = p.wwords - 1; }
+        int rcol = s0 + nact * VEC;
+        bool rvalid = true;
+        if (rcol >= p.wwords) { rvalid = p.wrap_x != 0; rcol = 0; }
+        const int ecol = lane == 0 ? lcol : rcol;  // lane 0: left edge, others: right edge
+        uint32_t cmask[VEC], omask[VEC], emask = 0xFFFFFFFFu;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            cmask[j] = CLIPPED ? col_mask(p.vis_cols, col + j) : 0xFFFFFFFFu;
+            omask[j] = CLIPPED ? col_mask(p.width, col + j) : 0xFFFFFFFFu;
+        }
+        if constexpr (CLIPPED) {
+            const uint32_t lm = lvalid ? col_mask(p.vis_cols, lcol) : 0u;
+            const uint32_t rm = rvalid ? col_mask(p.vis_cols, rcol) : 0u;
+            emask = lane == 0 ? lm : rm;
+        }
+        uint32_t lk1[VEC], lk2[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            lk1[j] = (uint32_t)(col + j) * kHashK1;
+            lk2[j] = (uint32_t)(col + j) * kHashK2;
+        }
+        const bool up = (bandi & 1) != 0;
+        // t-th stream row (t = 0 .. nrows+1) and i-th output row.
+        auto row_of = [&](int t) -> int { return up ? r_end - t : r_begin - 1 + t; };
+        auto out_of = [&](int i) -> int { return up ? r_end - 1 - i : r_begin + i; };
+
+        // Ring of stream rows: the lane's VEC words + its edge word.  The edge
+        // word rides the in-order vector memory pipe so the counted vmcnt
+        // waits cover it like the row data (a scalar load would need an
+        // out-of-order lgkmcnt(0) wait on every row).
+        Words<VEC> ring[kRing];
+        uint32_t edge[kRing];
+        auto load_t = [&](int t, Words<VEC>& d, uint32_t& e) {
+            const uint32_t* rp = row_ptr(p, row_of(t), 1);
+            load_words<VEC>(rp, lcolumn, d);
+            e = rp[ecol];
+        };
+        auto step_i = [&](int i, int u, bool in_band) {
+            const int ua = u % kRing, uc = (u + 1) % kRing, ub = (u + 2) % kRing;
+            const bool va = row_visible<CLIPPED>(p, row_of(i));
+            const bool vc = row_visible<CLIPPED>(p, row_of(i + 1));
+            const bool vb = row_visible<CLIPPED>(p, row_of(i + 2));
+            uint32_t v0[VEC], v1[VEC], cv[VEC];
+            column_sums<VEC, CLIPPED>(ring[ua], ring[uc], ring[ub], va, vc, vb, cmask, v0, v1, cv);
+            uint32_t eA = edge[ua], eC = edge[uc], eB = edge[ub];
+            if constexpr (CLIPPED) {
+                eA = va ? (eA & emask) : 0u;
+                eC = vc ? (eC & emask) : 0u;
+                eB = vb ? (eB & emask) : 0u;
+            }
+            const uint32_t te = eA ^ eC;
+            const uint32_t ev0 = te ^ eB, ev1 = bfi(te, eB, eA);
+            // Left / right neighbour column sums: the adjacent lane's, or --
+            // where DPP has no source lane -- `old`, this lane's edge word.
+            const uint32_t m0 = dpp_shr1(ev0, v0[VEC - 1]);
+            const uint32_t m1 = dpp_shr1(ev1, v1[VEC - 1]);
+            uint32_t n0 = dpp_shl1(ev0, v0[0]);
+            uint32_t n1 = dpp_shl1(ev1, v1[0]);
+            if (nact < kWaveLanes) {  // narrow strip: the last active lane is not lane 63
+                const uint32_t r0 = __builtin_amdgcn_readlane(ev0, 1);  // lane 1 holds the right edge
+                const uint32_t r1 = __builtin_amdgcn_readlane(ev1, 1);
+                const bool last = lane == nact - 1;
+                n0 = last ? r0 : n0;
+                n1 = last ? r1 : n1;
+            }
+            Words<VEC> o;
+            rule_words<VEC, LIFE>(p, v0, v1, m0, m1, n0, n1, ring[uc], cv, o);
+            if constexpr (CLIPPED) {
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
+            }
+            if (in_band) {
+                const int r = out_of(i);
+                store_words<VEC>(p.nxt + (int64_t)r * p.pitch, col, active, o);
+                if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc);
+            }
+        };
+
+        // Loads are never predicated: stream rows past the band's last one
+        // are clamped to it, and steps past the band compute into the void
+        // (their stores are skipped), so the loop body is straight-line.
+        const int tmax = nrows + 1;
+#pragma unroll
+        for (int t = 0; t < kRing - 1; ++t) load_t(min(t, tmax), ring[t], edge[t]);
+        for (int i0 = 0; i0 < nrows; i0 += kRing) {
+#pragma unroll
+            for (int u = 0; u < kRing; ++u) {
+                const int i = i0 + u;
+                const int sl = (u + kRing - 1) % kRing;
+                load_t(min(i + kRing - 1, tmax), ring[sl], edge[sl]);
+                step_i(i, u, i < nrows);
+            }
+        }
+        if (!active) acc = 0;
+    }
+    if constexpr (HASH) hash_flush(acc, p.hash_slots, lane, wave_in_wg);
+}
+
+// --------------------------------------------------------------------------
+// G generations per pass (temporal blocking).
+// --------------------------------------------------------------------------
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(const StepParams p) {
+    static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
+    static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
+    constexpr int kOut = (kWaveLanes - 2) * VEC;  // output words per strip
+    const int lane = threadIdx.x & (kWaveLanes - 1);
+    const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
+    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
+    const int rg = blockIdx.y;
+    const int strip = wave % p.strips;
+    const int bandi = wave / p.strips;
+    unsigned long long acc[G];
+#pragma unroll
+    for (int s = 0; s < G; ++s) acc[s] = 0;
+
+    if (bandi < p.nbands[rg]) {
+        const int r_begin = p.row_lo[rg] + bandi * p.band;
+        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int nrows = r_end - r_begin;
+        const int n_in = nrows + 2 * G;  // stream rows r_begin-G .. r_end+G-1
+        const int s0 = strip * kOut;
+        const int nout = min(kOut, p.wwords - s0);
+        const int col = s0 + (lane - 1) * VEC;  // lane 0: the strip's left halo
+        const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
+        int lcol;
+        bool incol;
+        if (p.wrap_x) {
+            lcol = col % p.wwords;
+            if (lcol < 0) lcol += p.wwords;
+            incol = true;
+        } else {
+            incol = col >= 0 && col < p.wwords;
+            lcol = incol ? col : 0;
+        }
+        uint32_t cmask[VEC], omask[VEC], lk1[VEC], lk2[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
+            omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
+            lk1[j] = (uint32_t)(col + j) * kHashK1;
+            lk2[j] = (uint32_t)(col + j) * kHashK2;
+        }
+        const bool up = (bandi & 1) != 0;
+        // stream row m <-> local board row (the same for every stage)
+        auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
+        auto vis = [&](int m) -> bool { return row_visible<CLIPPED>(p, brow(m)); };
+
+        Words<VEC> in[kMRing];
+        Words<VEC> st[G - 1][3];  // stage s (1..G-1) rows, slot = stream row % 3
+#pragma unroll
+        for (int k = 0; k < kMRing; ++k)
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) in[k].w[j] = 0u;
+#pragma unroll
+        for (int s = 0; s < G - 1; ++s)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) st[s][k].w[j] = 0u;
+
+        auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
+        // one stencil application: rows above/centre/below -> out
+        auto apply = [&](const Words<VEC>& A, const Words<VEC>& C, const Words<VEC>& B, int mc,
+                         Words<VEC>& o) {
+            uint32_t v0[VEC], v1[VEC], cv[VEC];
+            column_sums<VEC, CLIPPED>(A, C, B, vis(mc - 1), vis(mc), vis(mc + 1), cmask, v0, v1, cv);
+            // halo lanes 0 / 63 get garbage (0) beyond their outer edge
+            const uint32_t m0 = dpp_shr1(0u, v0[VEC - 1]);
+            const uint32_t m1 = dpp_shr1(0u, v1[VEC - 1]);
+            const uint32_t n0 = dpp_shl1(0u, v0[0]);
+            const uint32_t n1 = dpp_shl1(0u, v1[0]);
+            rule_words<VEC, LIFE>(p, v0, v1, m0, m1, n0, n1, C, cv, o);
+            if constexpr (CLIPPED) {
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
+            }
+        };
+
+#pragma unroll
+        for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
+        for (int q0 = 0; q0 < n_in; q0 += kMRing) {
+#pragma unroll
+            for (int u = 0; u < kMRing; ++u) {
+                const int q = q0 + u;
+                load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
+                // stage 1: stream row q-1 from input rows q-2, q-1, q
+                Words<VEC> o;
+                apply(in[(u + kMRing - 2) % kMRing], in[(u + kMRing - 1) % kMRing], in[u], q - 1, o);
+#pragma unroll
+                for (int s = 1; s <= G; ++s) {
+                    const int m = q - s;  // stream row produced by stage s
+                    const bool own_row = m >= G && m < n_in - G;
+                    if (s < G) {
+                        st[s - 1][((u - s) % 3 + 3) % 3] = o;
+                        if constexpr (HASH) {
+                            if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                        }
+                        // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
+                        apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
+                              st[s - 1][((u - s) % 3 + 3) % 3], m - 1, o);
+                    } else if (own_row) {
+                        const int r = brow(m);
+                        store_words<VEC>(p.nxt + (int64_t)r * p.pitch, lcol, owns, o);
+                        if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                    }
+                }
+            }
+        }
+        if (!owns) {
+#pragma unroll
+            for (int s = 0; s < G; ++s) acc[s] = 0;
+        }
+    }
+    if constexpr (HASH) {
+#pragma unroll
+        for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
+    }
+}
+
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
+    if constexpr (G == 1) {
+        hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+    } else {
+        hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+    }
+    return hipGetLastError();
+}
+
+template <int VEC, int G>
+hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, int gx, int gy,
+                          hipStream_t st) {
+    if (clipped) {
+        return hash ? launch_one<VEC, G, false, true, true>(p, gx, gy, st)
+                    : launch_one<VEC, G, false, false, true>(p, gx, gy, st);
+    }
+    if (life) {
+        return hash ? launch_one<VEC, G, true, true, false>(p, gx, gy, st)
+                    : launch_one<VEC, G, true, false, false>(p, gx, gy, st);
+    }
+    return hash ? launch_one<VEC, G, false, true, false>(p, gx, gy, st)
+                : launch_one<VEC, G, false, false, false>(p, gx, gy, st);
+}
+
+template <int G>
+hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool clipped, int gx, int gy,
+                       hipStream_t st) {
+    switch (vec) {
+        case 4: return launch_variant<4, G>(p, life, hash, clipped, gx, gy, st);
+        case 2: return launch_variant<2, G>(p, life, hash, clipped, gx, gy, st);
+        case 1: return launch_variant<1, G>(p, life, hash, clipped, gx, gy, st);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace dev
+
+// Defined one per translation unit (gol_step_g<G>.hip).
+hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+
+}  // namespace gol

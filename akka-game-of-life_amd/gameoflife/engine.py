@@ -130,10 +130,11 @@ class GolEngine:
     def profile(self, enable: bool = True) -> None:
         self._chk(N.lib.gol_profile_enable(self._h, 1 if enable else 0))
 
-    def profile_read(self) -> tuple[float, int]:
-        ms, n = ctypes.c_double(0), ctypes.c_uint64(0)
-        self._chk(N.lib.gol_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
-        return ms.value, n.value
+    def profile_read(self) -> tuple[float, int, int]:
+        """(kernel ms, launches, generations advanced by those launches)."""
+        ms, n, g = ctypes.c_double(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._chk(N.lib.gol_profile_read(self._h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(g)))
+        return ms.value, n.value, g.value
 
     def profile_reset(self) -> None:
         self._chk(N.lib.gol_profile_reset(self._h))

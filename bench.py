@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CELL_UPDATE = 0.25
+DEFAULT_GPP = 2  # generations per HBM pass (scripts/tune.py sweep; DESIGN.md "Measurement")
 
 
 def parse():
@@ -38,6 +39,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
     ap.add_argument("--band", type=int, default=0, help="rows per band (0 = auto)")
+    ap.add_argument("--gpp", type=int, default=DEFAULT_GPP,
+                    help="generations fused per HBM pass (temporal blocking depth, 1..4)")
     ap.add_argument("--hash", action="store_true", help="fuse the per-generation state hash")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -77,13 +80,13 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
     torch.cuda.synchronize()
     barrier(dist, world)
     dt = time.perf_counter() - t0
-    kms, launches = eng.profile_read()
+    kms, launches, gens = eng.profile_read()
     eng.profile(False)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    return dt, kms, launches
+    return dt, kms, launches, gens
 
 
 def cpu_baseline(width, seconds):
@@ -106,6 +109,32 @@ def cpu_baseline(width, seconds):
                       f"the same workload, {gens} generations in {dt:.1f} s, {threads} OpenMP threads"}
 
 
+def roofline(kms, launches, gens_covered, cells_per_gen_per_launch):
+    """Algorithmic bytes per launch (0.25 B per cell-update x cells x the
+    generations one launch advances) / the launch's average duration."""
+    if not launches:
+        return None
+    avg_s = kms / 1e3 / launches
+    gpl = gens_covered / launches
+    algo = cells_per_gen_per_launch * gpl * BYTES_PER_CELL_UPDATE
+    ach = algo / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
+            "generations_per_launch": gpl, "algorithmic_bytes_per_launch": algo}
+
+
+def pmc_traffic(workload_key):
+    """HBM bytes per launch measured with rocprofv3 --pmc (profiles/pmc_traffic.json,
+    written by scripts/pmc_traffic.py with the gfx950 FETCH_SIZE x2 correction)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     a = parse()
     torch, dist, rank, world, local = dist_setup(a.gpus)
@@ -115,8 +144,7 @@ def main():
     W = H = a.board
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
-    if a.band:
-        eng.set_tuning(band_rows=a.band)
+    eng.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
     if world > 1:
         uid = N.unique_id() if rank == 0 else bytes(N.GOL_UNIQUE_ID_BYTES)
         t = torch.tensor(list(uid), dtype=torch.uint8)
@@ -124,12 +152,20 @@ def main():
         eng.comm_init(bytes(t.tolist()), rank, world)
     eng.seed(0x5EED)
 
-    dt, kms, launches = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
     value = W * H * a.steps / dt / 1e9
-    # dominant kernel: the full-shard (N=1) or interior (N>1) step launch
-    cells_per_launch = W * (rows if world == 1 else max(rows - 2, 0))
-    avg_s = kms / 1e3 / max(launches, 1)
-    achieved = cells_per_launch * BYTES_PER_CELL_UPDATE / avg_s / 1e9 if launches else None
+    # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a pass
+    G = a.gpp
+    cells = W * (rows if world == 1 else max(rows - 2 * G, 0))
+    roof = roofline(kms, launches, gcov, cells)
+    key = f"{W}x{H}/N{world}/G{G}/band{a.band}"
+    if roof is not None:
+        roof["kernel"] = ("gol::dev::step_kernel<4,LIFE>" if G == 1
+                          else f"gol::dev::multistep_kernel<4,{G},LIFE>")
+        t = pmc_traffic(key)
+        if t is not None:
+            roof["traffic"] = t.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = t.get("source")
     out = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 2),
@@ -141,21 +177,15 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u32 (bit-packed cells)",
+        "dtype": "u32 (bit-packed cells, bitwise ops)",
         "data": "synthetic (splitmix64 Bernoulli(0.5) board, seed 0x5EED)",
         "config": {"workload": f"{W}x{H} torus B3/S23 row-sharded over {world} GPU(s) "
                                f"(BASELINE.json configs[3]; N=1 = whole board on one GPU)",
                    "board": [W, H], "rule": "B3/S23", "topology": "torus",
                    "parallelism": f"row-block x{world}, RCCL halo send/recv",
+                   "generations_per_pass": G, "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash)},
-        "roofline": {"bound": "hbm",
-                     "achieved": round(achieved, 1) if achieved else None,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": None,
-                     "kernel": "gol::step_kernel<VEC=4,LIFE,...>",
-                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
-                     "algorithmic_bytes_per_launch": cells_per_launch * BYTES_PER_CELL_UPDATE},
+        "roofline": roof,
     }
     eng.close()
 
@@ -163,17 +193,20 @@ def main():
         if not a.no_secondary:
             S = 65536
             with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
+                e2.set_tuning(band_rows=a.band, gens_per_pass=G)
                 e2.seed(0x5EED)
-                dt2, kms2, n2 = timed_run(e2, torch, dist, 1, max(a.steps, 20), a.warmup, a.hash)
-                avg2 = kms2 / 1e3 / max(n2, 1)
-                ach2 = S * S * BYTES_PER_CELL_UPDATE / avg2 / 1e9
+                n2 = max(a.steps, 24)
+                dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, a.warmup, a.hash)
+                r2 = roofline(kms2, l2, g2, S * S)
+                if r2 is not None:
+                    t = pmc_traffic(f"{S}x{S}/N1/G{G}/band{a.band}")
+                    if t is not None:
+                        r2["traffic"] = t.get("hbm_bytes_per_launch")
+                        r2["traffic_source"] = t.get("source")
                 out["secondary"] = {
                     "workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
-                    "value": round(S * S * max(a.steps, 20) / dt2 / 1e9, 2), "unit": "GCUPS",
-                    "ms_per_step": round(dt2 / max(a.steps, 20) * 1e3, 4),
-                    "roofline": {"achieved": round(ach2, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(ach2 / HBM_PEAK_GBS, 4),
-                                 "avg_launch_ms": round(avg2 * 1e3, 4)}}
+                    "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS",
+                    "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2}
         if not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
     if rank == 0:

@@ -163,15 +163,18 @@ int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank,
  * place (the per-generation hash reduction). */
 int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count);
 
-/* Kernel timing: when enabled, every step-kernel launch is bracketed by HIP
- * events on the stream it runs on.  gol_profile_read returns the summed
- * duration (ms) and the number of launches since the last reset. */
+/* Kernel timing: when enabled, the dominant step-kernel launch of every pass
+ * (the whole shard, or a sharded shard's interior rows) is bracketed by HIP
+ * events on the stream it runs on.  gol_profile_read returns, since the last
+ * reset, the summed duration (ms), the number of launches and the number of
+ * generations those launches advanced (a pass may fuse several). */
 int gol_profile_enable(gol_ctx* ctx, int enable);
-int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches);
+int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* generations);
 int gol_profile_reset(gol_ctx* ctx);
 
-/* Tuning knobs (0 = automatic): rows per band streamed by one wave, and the
- * number of generations fused per pass (temporal blocking; 1 = none). */
+/* Tuning knobs: rows per band streamed by one wave (0 = automatic), and the
+ * number of generations fused per HBM pass (temporal blocking, 1..4; 0 keeps
+ * the current value; default 1).  Results do not depend on either. */
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass);
 
 /* Diagnostic: runs a one-wave kernel exercising the cross-lane primitives the

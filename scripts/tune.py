@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Sweep of pass depth G (generations per HBM pass) x band size for the step
+kernel: interleaved rounds in one process, kernel time from HIP events.
+
+    python scripts/tune.py [edge ...]      env: BANDS=0,16,...  GPPS=1,2,3,4  ROUNDS=3
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
+
+from gameoflife.engine import GolEngine  # noqa: E402
+
+
+def measure(e, gens, hashes=False):
+    e.profile(True)
+    e.profile_reset()
+    t0 = time.perf_counter()
+    e.step(gens, hashes=hashes)
+    e.sync()
+    wall = time.perf_counter() - t0
+    ms, n, g = e.profile_read()
+    e.profile(False)
+    return ms / max(g, 1), wall / gens * 1e3  # kernel ms per generation, wall ms per generation
+
+
+def main():
+    edges = [int(a) for a in sys.argv[1:]] or [65536, 262144]
+    bands = [int(b) for b in os.environ.get("BANDS", "0,16,32,64,128,256").split(",")]
+    gpps = [int(g) for g in os.environ.get("GPPS", "1,2,3,4").split(",")]
+    rounds = int(os.environ.get("ROUNDS", "3"))
+    for edge in edges:
+        gens = 48 if edge <= 65536 else 12
+        with GolEngine(edge, edge) as e:
+            e.seed(0x5EED)
+            e.step(3)
+            keys = [(g, b) for g in gpps for b in bands]
+            res = {k: [] for k in keys}
+            resh = {k: [] for k in keys}
+            for _ in range(rounds):
+                for (g, b) in keys:
+                    e.set_tuning(band_rows=b, gens_per_pass=g)
+                    res[(g, b)].append(measure(e, gens))
+                    resh[(g, b)].append(measure(e, gens, hashes=True))
+            bytes_per_gen = edge * edge * 0.25
+            for (g, b) in keys:
+                k = min(x[0] for x in res[(g, b)])
+                w = min(x[1] for x in res[(g, b)])
+                kh = min(x[0] for x in resh[(g, b)])
+                print(f"edge={edge} G={g} band={b:5d} kernel_ms/gen={k:.4f} wall_ms/gen={w:.4f} "
+                      f"GCUPS={edge * edge / k / 1e6:9.1f} frac={bytes_per_gen / k / 1e6 / 8000:.3f} | "
+                      f"hash: kernel_ms/gen={kh:.4f} frac={bytes_per_gen / kh / 1e6 / 8000:.3f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,15 +27,17 @@ def rule_obj(rule):
     return Rule(rule[0], rule[1])
 
 
-def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0):
+GPP = [1, 2, 3, 4]  # generations fused per HBM pass (temporal blocking depth)
+
+
+def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0, gpp=1):
     topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
     if cells is not None:
         board = O.pack(cells)
     else:
         board = O.seed_packed(W, H, seed if seed is not None else 0x5EED)
     with engine(W, H, topology=topology, rule=rule_obj(rule)) as e:
-        if band:
-            e.set_tuning(band_rows=band)
+        e.set_tuning(band_rows=band, gens_per_pass=gpp)
         e.load(board)
         assert e.hash() == O.hash_packed(board, W)
         got = e.step(gens, hashes=True)
@@ -76,58 +78,72 @@ TORUS_SHAPES = [(32, 8), (64, 3), (96, 17), (32 * 63, 5), (32 * 64, 9), (32 * 12
                 (32 * 130, 11), (32 * 256, 33), (32 * 260, 7), (32 * 1024, 70), (32 * 2048, 4)]
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("W,H", TORUS_SHAPES)
-def test_torus_life(gpu, W, H):
-    check_run(W, H, 12, O.LIFE, "torus", seed=W * 7 + H)
+def test_torus_life(gpu, W, H, gpp):
+    check_run(W, H, 12, O.LIFE, "torus", seed=W * 7 + H, gpp=gpp)
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("H", [1, 2, 3])
-def test_torus_tiny_heights(gpu, H):
+def test_torus_tiny_heights(gpu, H, gpp):
     # rows alias on a torus shorter than 3 rows (multiset count)
-    check_run(32 * 8, H, 6, O.LIFE, "torus", seed=H)
-    check_run(32 * 8, H, 6, (0x1A4, 0x03B), "torus", seed=H)
+    check_run(32 * 8, H, 6, O.LIFE, "torus", seed=H, gpp=gpp)
+    check_run(32 * 8, H, 6, (0x1A4, 0x03B), "torus", seed=H, gpp=gpp)
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("band", [1, 2, 3, 5, 7, 16, 1000])
-def test_band_sizes(gpu, band):
+def test_band_sizes(gpu, band, gpp):
     # short bands exercise the boustrophedon direction switch and ring tails
-    check_run(32 * 256, 61, 5, O.LIFE, "torus", seed=band, band=band)
-    check_run(32 * 4, 23, 5, (0x049, 0x16E), "torus", seed=band, band=band)
+    check_run(32 * 256, 61, 7, O.LIFE, "torus", seed=band, band=band, gpp=gpp)
+    check_run(32 * 4, 23, 7, (0x049, 0x16E), "torus", seed=band, band=band, gpp=gpp)
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("seed", range(6))
-def test_torus_random_rules(gpu, seed):
+def test_torus_random_rules(gpu, seed, gpp):
     rng = np.random.default_rng(seed)
     rule = (int(rng.integers(0, 512)), int(rng.integers(0, 512)))
     W = 32 * int(rng.choice([1, 3, 64, 130, 256, 300]))
     H = int(rng.integers(1, 50))
-    check_run(W, H, 8, rule, "torus", seed=seed)
+    check_run(W, H, 8, rule, "torus", seed=seed, gpp=gpp)
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("name", list(RULES))
-def test_torus_named_rules(gpu, name):
-    check_run(32 * 96, 31, 10, RULES[name], "torus", seed=3)
+def test_torus_named_rules(gpu, name, gpp):
+    check_run(32 * 96, 31, 10, RULES[name], "torus", seed=3, gpp=gpp)
+
+
+@pytest.mark.parametrize("gpp", GPP)
+def test_gens_not_multiple_of_depth(gpu, gpp):
+    # remainder passes run at a shallower depth; hashes stay per generation
+    for gens in (1, 5, 7, 13):
+        check_run(32 * 300, 45, gens, O.LIFE, "torus", seed=gens, gpp=gpp)
 
 
 CLIPPED_SHAPES = [(7, 7), (2, 2), (33, 40), (100, 65), (32, 9), (1000, 37), (32 * 300 + 5, 12),
                   (64 * 32 + 1, 20)]
 
 
+@pytest.mark.parametrize("gpp", GPP)
 @pytest.mark.parametrize("W,H", CLIPPED_SHAPES)
 @pytest.mark.parametrize("name", list(RULES))
-def test_ref_clipped(gpu, W, H, name):
+def test_ref_clipped(gpu, W, H, name, gpp):
     rng = np.random.default_rng(W * 31 + H)
     cells = (rng.random((H, W)) < 0.45).astype(np.uint8)
-    check_run(W, H, 6, RULES[name], "ref-clipped", cells=cells)
+    check_run(W, H, 6, RULES[name], "ref-clipped", cells=cells, gpp=gpp)
 
 
-def test_ref_clipped_random_rules(gpu):
+@pytest.mark.parametrize("gpp", GPP)
+def test_ref_clipped_random_rules(gpu, gpp):
     rng = np.random.default_rng(99)
     for _ in range(6):
         rule = (int(rng.integers(0, 512)), int(rng.integers(0, 512)))
         W, H = int(rng.integers(2, 400)), int(rng.integers(2, 60))
         cells = (rng.random((H, W)) < 0.5).astype(np.uint8)
-        check_run(W, H, 5, rule, "ref-clipped", cells=cells)
+        check_run(W, H, 5, rule, "ref-clipped", cells=cells, gpp=gpp)
 
 
 def test_golden_ref_default_board(gpu):
@@ -138,20 +154,24 @@ def test_golden_ref_default_board(gpu):
         cells = np.array([[int(ch) for ch in row] for row in entry["initial"]], dtype=np.uint8)
         assert (cells == O.java_random_cells(w, h, entry["java_seed"])).all()
         for name, res in entry["modes"].items():
-            with engine(w + 1, h + 1, topology="ref-clipped", rule=name) as e:
-                e.load(O.pack(cells))
-                got = e.step(100, hashes=True)
-                assert [int(x) for x in got] == res["hashes"], (entry["java_seed"], name)
-                final = O.unpack(e.snapshot(), w + 1)
-                want = np.array([[int(ch) for ch in row] for row in res["boards"][-1]["cells"]])
-                assert (final == want).all()
+            for gpp in GPP:
+                with engine(w + 1, h + 1, topology="ref-clipped", rule=name) as e:
+                    e.set_tuning(gens_per_pass=gpp)
+                    e.load(O.pack(cells))
+                    got = e.step(100, hashes=True)
+                    assert [int(x) for x in got] == res["hashes"], (entry["java_seed"], name, gpp)
+                    final = O.unpack(e.snapshot(), w + 1)
+                    want = np.array([[int(ch) for ch in row] for row in res["boards"][-1]["cells"]])
+                    assert (final == want).all()
 
 
-def test_golden_torus_4096_1000(gpu):
+@pytest.mark.parametrize("gpp", GPP)
+def test_golden_torus_4096_1000(gpu, gpp):
     """BASELINE.json config 2: 4096^2 torus B3/S23, 1000 generations,
     per-generation hashes bit-exact against the committed oracle vectors."""
     for g in GOLDEN["torus"]:
         with engine(g["W"], g["H"], topology="torus", rule=g["rule"]) as e:
+            e.set_tuning(gens_per_pass=gpp)
             e.seed(g["seed"])
             assert e.hash() == g["hash0"]
             got = e.step(g["gens"], hashes=True)
@@ -189,14 +209,16 @@ def test_full_size_65536_bit_exact(gpu):
     """BASELINE.json config 3 geometry (65536^2 torus): 3 generations checked
     word-for-word against the multithreaded CPU oracle."""
     W = H = 65536
-    with engine(W, H) as e:
-        e.seed(0x5EED)
-        got = e.step(3, hashes=True)
-        final = e.snapshot()
     board = O.seed_packed(W, H, 0x5EED)
-    final_cpu, want = O.run_packed(board, W, 3, O.TORUS, O.LIFE)
-    np.testing.assert_array_equal(got, want)
-    assert (final == final_cpu).all()
+    final_cpu, want = O.run_packed(board, W, 4, O.TORUS, O.LIFE)
+    for gpp in (1, 2, 4):
+        with engine(W, H) as e:
+            e.set_tuning(gens_per_pass=gpp)
+            e.seed(0x5EED)
+            got = e.step(4, hashes=True)
+            final = e.snapshot()
+        np.testing.assert_array_equal(got, want)
+        assert (final == final_cpu).all(), gpp
 
 
 def test_known_patterns_on_gpu(gpu):

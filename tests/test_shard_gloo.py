@@ -1,0 +1,108 @@
+"""Multi-rank path on CPU (world_size 2 and 3, gloo): row-block shards that
+exchange halo rows in exactly libgol's op order (shard.HaloPlan) and reduce
+per-generation partial hashes must reproduce the unsharded board and hashes.
+The compute here is the oracle (test double for the GPU); what is under test
+is the decomposition, the halo protocol and the hash reduction."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gameoflife.shard import HaloPlan, combine_hashes, shard_rows_py
+from oracle import oracle as O
+
+W, H, GENS = 32 * 9, 37, 12
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _exchange(plan: HaloPlan, shard: np.ndarray):
+    """Issue the plan's ops as gloo isend/irecv (one 'group')."""
+    reqs, recv = [], {}
+    zero = np.zeros(shard.shape[1], dtype=np.uint32)
+    for kind, what, peer in plan.ops():
+        if kind == "send":
+            row = shard[-1] if what == "last" else shard[0]
+            reqs.append(dist.isend(torch.from_numpy(row.astype(np.int32).copy()), peer))
+        else:
+            buf = torch.zeros(shard.shape[1], dtype=torch.int32)
+            reqs.append(dist.irecv(buf, peer))
+            recv[what] = buf
+    for r in reqs:
+        r.wait()
+    top = recv["top"].numpy().astype(np.uint32) if "top" in recv else zero
+    bot = recv["bot"].numpy().astype(np.uint32) if "bot" in recv else zero
+    return top, bot
+
+
+def _worker(rank, world, port, torus, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        row0, rows = shard_rows_py(H, rank, world)
+        full = O.seed_packed(W, H, 1234)
+        shard = full[row0:row0 + rows].copy()
+        plan = HaloPlan(rank, world, torus)
+        hashes = []
+        for _ in range(GENS):
+            top, bot = _exchange(plan, shard)
+            ext = np.vstack([top[None], shard, bot[None]])
+            if torus:
+                nxt = O.step_packed(ext, W, O.TORUS, O.LIFE)[1:-1]
+            else:
+                # clipped geometry, visible region = global [0,W-1) x [0,H-1)
+                # ext row k is global row row0-1+k; visible iff global < H-1
+                nxt = O.step_packed(ext, W, O.REF_CLIPPED, O.LIFE, vis=(W - 1, H - row0))[1:-1]
+            shard = nxt
+            part = O.hash_packed(shard, W, row0=row0)
+            t = torch.tensor([part - (1 << 64) if part >= (1 << 63) else part], dtype=torch.int64)
+            dist.all_reduce(t)  # int64 sum wraps like uint64
+            hashes.append(int(t.item()) & ((1 << 64) - 1))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (row0, shard.tolist()))
+        if rank == 0:
+            out_q.put((hashes, gathered))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,torus", [(2, True), (3, True), (2, False), (3, False)])
+def test_sharded_matches_unsharded(world, torus):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, torus, q), nprocs=world, start_method="spawn")
+    hashes, gathered = q.get(timeout=60)
+    board = np.vstack([np.array(s, dtype=np.uint32) for _, s in sorted(gathered)])
+    topo = O.TORUS if torus else O.REF_CLIPPED
+    ref, ref_h = O.run_packed(O.seed_packed(W, H, 1234), W, GENS, topo, O.LIFE)
+    assert (board == ref).all()
+    assert hashes == [int(x) for x in ref_h]
+
+
+def test_halo_plan_two_ranks_pairs_rows_correctly():
+    """With 2 ranks up == down; per-peer FIFO order must pair the sender's
+    last row with the receiver's top halo."""
+    p0, p1 = HaloPlan(0, 2, True), HaloPlan(1, 2, True)
+    sends0 = [w for k, w, _ in p0.ops() if k == "send"]
+    recvs1 = [w for k, w, _ in p1.ops() if k == "recv"]
+    assert sends0 == ["last", "first"] and recvs1 == ["top", "bot"]
+    # clipped: the ends of the ring do not wrap
+    assert HaloPlan(0, 3, False).ops() == [("send", "last", 1), ("recv", "bot", 1)]
+    assert HaloPlan(2, 3, False).ops() == [("send", "first", 1), ("recv", "top", 1)]
+
+
+def test_combine_hashes_wraps_mod_2_64():
+    a = np.array([2**64 - 1, 5], dtype=np.uint64)
+    b = np.array([2, 7], dtype=np.uint64)
+    assert combine_hashes([a, b]).tolist() == [1, 12]
