@@ -57,6 +57,13 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {
 __device__ __forceinline__ uint32_t dpp_shl1(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kDppWaveShl1, 0xf, 0xf, false);
 }
+// Same shifts with zeros where there is no source lane (no `old` operand).
+__device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppWaveShr1, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t dpp_shl1_zero(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppWaveShl1, 0xf, 0xf, true);
+}
 
 // Bits [0, limit) of word `w` set (limit in cells).
 __device__ __forceinline__ uint32_t col_mask(int64_t limit, int64_t w) {
@@ -122,11 +129,22 @@ __device__ __forceinline__ bool row_visible(const StepParams& p, int r) {
     }
 }
 
-// Vertical 3-sums (v1 v0) = a + c + b of the visible rows.
+// v_bitop3_b32 truth tables: imm = f(S0 = 0xF0, S1 = 0xCC, S2 = 0xAA).
+constexpr uint32_t kXor3 = 0x96;         // a ^ b ^ c
+constexpr uint32_t kMaj = 0xE8;          // majority(a, b, c)
+constexpr uint32_t kNotAXorBC = 0x06;    // ~a & (b ^ c)
+constexpr uint32_t kAAndBOrC = 0xE0;     // a & (b | c)
+
+#define GOL_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
+
+// Column sums of the visible rows: (v1 v0) = a + c + b (the full 3-cell
+// column, seen by the columns left and right of it) and (p1 p0) = a + b (the
+// column minus its centre, seen by the centre cell itself).
 template <int VEC, bool CLIPPED>
 __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC>& C, const Words<VEC>& B,
                                             bool va, bool vc, bool vb, const uint32_t (&cmask)[VEC],
-                                            uint32_t (&v0)[VEC], uint32_t (&v1)[VEC], uint32_t (&cv)[VEC]) {
+                                            uint32_t (&v0)[VEC], uint32_t (&v1)[VEC], uint32_t (&p0)[VEC],
+                                            uint32_t (&p1)[VEC]) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
         uint32_t a = A.w[j], c = C.w[j], b = B.w[j];
@@ -135,52 +153,49 @@ __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC
             c = vc ? (c & cmask[j]) : 0u;
             b = vb ? (b & cmask[j]) : 0u;
         }
-        const uint32_t t = a ^ c;
-        v0[j] = t ^ b;
-        v1[j] = bfi(t, b, a);
-        cv[j] = c;
+        v0[j] = GOL_BITOP3(a, c, b, kXor3);
+        v1[j] = GOL_BITOP3(a, c, b, kMaj);
+        p0[j] = a ^ b;
+        p1[j] = a & b;
     }
 }
 
-// The rule on one lane's VEC words given the column sums of its words and of
-// the words left (m0 m1) and right (n0 n1) of them.
+// The rule on one lane's VEC words from the column sums of its words, of the
+// word left of them (m0 m1) and of the word right of them (n0 n1).
+//   n = v(x-1) + v(x+1) + (a + b)(x)   -- the 8 neighbours, three 2-bit terms
+//   bit 0: n0 = xor3(w0, e0, p0), carry c0 = maj(w0, e0, p0)
+//   bit 1: weight-2 terms w1 + e1 + p1 = pp + 2 qq, pp = xor3, qq = maj
+//   n = n0 + 2 (pp + c0) + 4 qq
+// B3/S23: next = (n == 3) | (alive & n == 2) = ~qq & (pp ^ c0) & (n0 | alive)
+// (pp ^ c0 = 1 means exactly one of pp, c0 is set, so bit 2 is qq; n = 8 has
+// pp = c0 = 0 and dies) -- two v_bitop3 after the adder.
 template <int VEC, bool LIFE>
 __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (&v0)[VEC],
-                                           const uint32_t (&v1)[VEC], uint32_t m0, uint32_t m1,
-                                           uint32_t n0, uint32_t n1, const Words<VEC>& alive,
-                                           const uint32_t (&cv)[VEC], Words<VEC>& out) {
+                                           const uint32_t (&v1)[VEC], const uint32_t (&p0)[VEC],
+                                           const uint32_t (&p1)[VEC], uint32_t m0, uint32_t m1, uint32_t n0,
+                                           uint32_t n1, const Words<VEC>& alive, Words<VEC>& out) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-        const uint32_t p0 = j == 0 ? m0 : v0[j - 1];
-        const uint32_t p1 = j == 0 ? m1 : v1[j - 1];
-        const uint32_t q0 = j == VEC - 1 ? n0 : v0[j + 1];
-        const uint32_t q1 = j == VEC - 1 ? n1 : v1[j + 1];
-        const uint32_t w0 = __builtin_amdgcn_alignbit(v0[j], p0, 31);  // column x-1
-        const uint32_t e0 = __builtin_amdgcn_alignbit(q0, v0[j], 1);   // column x+1
-        const uint32_t w1 = __builtin_amdgcn_alignbit(v1[j], p1, 31);
-        const uint32_t e1 = __builtin_amdgcn_alignbit(q1, v1[j], 1);
-        // T9 = (w1 w0) + (v1 v0) + (e1 e0) = s3 s2 s1 s0
-        const uint32_t t0 = w0 ^ v0[j];
-        const uint32_t s0 = t0 ^ e0;
-        const uint32_t c0 = bfi(t0, e0, w0);
-        const uint32_t t1 = w1 ^ v1[j];
-        const uint32_t pp = t1 ^ e1;
-        const uint32_t qq = bfi(t1, e1, w1);
-        const uint32_t s1 = pp ^ c0;
-        const uint32_t r2 = pp & c0;
-        const uint32_t s2 = qq ^ r2;
+        const uint32_t l0 = j == 0 ? m0 : v0[j - 1];
+        const uint32_t l1 = j == 0 ? m1 : v1[j - 1];
+        const uint32_t r0 = j == VEC - 1 ? n0 : v0[j + 1];
+        const uint32_t r1 = j == VEC - 1 ? n1 : v1[j + 1];
+        const uint32_t w0 = __builtin_amdgcn_alignbit(v0[j], l0, 31);  // column x-1
+        const uint32_t e0 = __builtin_amdgcn_alignbit(r0, v0[j], 1);   // column x+1
+        const uint32_t w1 = __builtin_amdgcn_alignbit(v1[j], l1, 31);
+        const uint32_t e1 = __builtin_amdgcn_alignbit(r1, v1[j], 1);
+        const uint32_t nb0 = GOL_BITOP3(w0, e0, p0[j], kXor3);
+        const uint32_t c0 = GOL_BITOP3(w0, e0, p0[j], kMaj);
+        const uint32_t pp = GOL_BITOP3(w1, e1, p1[j], kXor3);
+        const uint32_t qq = GOL_BITOP3(w1, e1, p1[j], kMaj);
         const uint32_t al = alive.w[j];
         if constexpr (LIFE) {
-            // T9 mod 8 == 3, or alive and T9 mod 8 == 4 (T9 in {8,9} maps to {0,1}).
-            out.w[j] = bfi(s2, al & ~(s1 | s0), s1 & s0);
+            const uint32_t x = GOL_BITOP3(qq, pp, c0, kNotAXorBC);
+            out.w[j] = GOL_BITOP3(x, nb0, al, kAAndBOrC);
         } else {
-            const uint32_t s3 = qq & r2;
-            // n = T9 - visible centre (a 1-bit borrow chain).
-            const uint32_t c = cv[j];
-            const uint32_t n0b = s0 ^ c, b0 = c & ~s0;
-            const uint32_t n1b = s1 ^ b0, b1 = b0 & ~s1;
-            const uint32_t n2b = s2 ^ b1, b2 = b1 & ~s2;
-            const uint32_t n3b = s3 ^ b2;
+            const uint32_t n1b = pp ^ c0, k = pp & c0;
+            const uint32_t n2b = qq ^ k, n3b = qq & k;
+            const uint32_t n0b = nb0;
             uint32_t L[9];
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
@@ -298,8 +313,8 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const bool va = row_visible<CLIPPED>(p, row_of(i));
             const bool vc = row_visible<CLIPPED>(p, row_of(i + 1));
             const bool vb = row_visible<CLIPPED>(p, row_of(i + 2));
-            uint32_t v0[VEC], v1[VEC], cv[VEC];
-            column_sums<VEC, CLIPPED>(ring[ua], ring[uc], ring[ub], va, vc, vb, cmask, v0, v1, cv);
+            uint32_t v0[VEC], v1[VEC], p0[VEC], p1[VEC];
+            column_sums<VEC, CLIPPED>(ring[ua], ring[uc], ring[ub], va, vc, vb, cmask, v0, v1, p0, p1);
             uint32_t eA = edge[ua], eC = edge[uc], eB = edge[ub];
             if constexpr (CLIPPED) {
                 eA = va ? (eA & emask) : 0u;
@@ -322,7 +337,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 n1 = last ? r1 : n1;
             }
             Words<VEC> o;
-            rule_words<VEC, LIFE>(p, v0, v1, m0, m1, n0, n1, ring[uc], cv, o);
+            rule_words<VEC, LIFE>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -421,14 +436,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
         // one stencil application: rows above/centre/below -> out
         auto apply = [&](const Words<VEC>& A, const Words<VEC>& C, const Words<VEC>& B, int mc,
                          Words<VEC>& o) {
-            uint32_t v0[VEC], v1[VEC], cv[VEC];
-            column_sums<VEC, CLIPPED>(A, C, B, vis(mc - 1), vis(mc), vis(mc + 1), cmask, v0, v1, cv);
-            // halo lanes 0 / 63 get garbage (0) beyond their outer edge
-            const uint32_t m0 = dpp_shr1(0u, v0[VEC - 1]);
-            const uint32_t m1 = dpp_shr1(0u, v1[VEC - 1]);
-            const uint32_t n0 = dpp_shl1(0u, v0[0]);
-            const uint32_t n1 = dpp_shl1(0u, v1[0]);
-            rule_words<VEC, LIFE>(p, v0, v1, m0, m1, n0, n1, C, cv, o);
+            uint32_t v0[VEC], v1[VEC], p0[VEC], p1[VEC];
+            column_sums<VEC, CLIPPED>(A, C, B, vis(mc - 1), vis(mc), vis(mc + 1), cmask, v0, v1, p0, p1);
+            // halo lanes 0 / 63 read zeros beyond their outer edge (bound_ctrl)
+            const uint32_t m0 = dpp_shr1_zero(v0[VEC - 1]);
+            const uint32_t m1 = dpp_shr1_zero(v1[VEC - 1]);
+            const uint32_t n0 = dpp_shl1_zero(v0[0]);
+            const uint32_t n1 = dpp_shl1_zero(v1[0]);
+            rule_words<VEC, LIFE>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];

@@ -4,6 +4,6 @@ timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -p no:cach
 rc=$?
 echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 if [ $rc -eq 0 ]; then
-  timeout -k 10 600 python scripts/tune.py > gpurun_out/tune.log 2>&1
+  BANDS=0,64,128,256,512 timeout -k 10 600 python scripts/tune.py > gpurun_out/tune.log 2>&1
   echo "tune rc=$?"; cat gpurun_out/tune.log
 fi
