@@ -44,7 +44,7 @@ struct gol_ctx {
     uint32_t birth = 0, survive = 0;
     int64_t vis_w = 0, vis_h = 0;
     int device = 0;
-    int vec = 1;
+    int vec_fixed = 0;  // words per lane forced by gol_set_tuning (0: per-pass automatic)
     // device state
     uint32_t* plane[2] = {nullptr, nullptr};
     int cur = 0;
@@ -61,7 +61,8 @@ struct gol_ctx {
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
     // tuning
-    int32_t band_rows = 0, gens_per_pass = 1;  // gens_per_pass: temporal blocking depth
+    int32_t band_rows = 0;                                   // 0: automatic
+    int32_t gens_per_pass = 0;                               // temporal blocking depth (0: automatic)
     // profiling
     bool prof = false;
     std::vector<EventPair> evs;
@@ -163,15 +164,42 @@ EventPair* next_event_pair(gol_ctx* ctx) {
     return &ctx->evs[ctx->evs_used++];
 }
 
-int pick_band(const gol_ctx* ctx, int64_t rows, int strips) {
+// Automatic tuning (scripts/tune.py sweeps on MI355X, profiles/r01_*):
+// results never depend on these choices.
+constexpr int kAutoGensPerPass = 6;  // best depth at 65536^2 and 262144^2
+
+// Words per lane for a single-generation pass: 16-byte lane loads where the
+// row fills whole waves of them.
+int default_vec(int64_t wwords) {
+    return (wwords % 4 == 0 && wwords >= 256) ? 4 : (wwords % 2 == 0 && wwords >= 128) ? 2 : 1;
+}
+
+// Words per lane for a pass of `gens` generations.  Multi-generation strips
+// carry 62 output lanes, so a row of w words needs ceil(w / (62 v)) strips;
+// prefer 16-byte lanes unless 8-byte lanes waste clearly fewer lanes.
+int lane_words(const gol_ctx* ctx, int gens) {
+    if (ctx->vec_fixed > 0) return ctx->vec_fixed;
+    const int64_t w = ctx->wwords;
+    if (gens == 1) return default_vec(w);
+    auto util = [&](int v) -> double {
+        const int64_t strips = (w / v + 61) / 62;
+        return (double)(w / v) / (double)(strips * 64);
+    };
+    const bool ok4 = w % 4 == 0 && w >= 4 * 62, ok2 = w % 2 == 0 && w >= 2 * 62;
+    if (ok4 && (!ok2 || util(4) >= util(2) - 0.03)) return 4;
+    if (ok2) return 2;
+    return 1;
+}
+
+int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens) {
     if (ctx->band_rows > 0) return ctx->band_rows;
-    // Aim at ~8192 waves: one full residency round of 256-thread workgroups
-    // (8 per CU x 256 CUs x 4 waves) so all bands finish together.
-    const int64_t target_waves = 8192;
-    int64_t bands = std::max<int64_t>(1, target_waves / std::max(1, strips));
+    if (gens == 1) return 16;  // short bands: more waves in flight, seams hit the Infinity Cache
+    // Multi-generation passes recompute 2G halo rows per band: keep bands
+    // >= 64 rows, aim at ~8192 waves, cap at 256 rows.
+    const int64_t bands = std::max<int64_t>(1, 8192 / std::max(1, strips));
     int64_t band = (rows + bands - 1) / bands;
-    band = std::max<int64_t>(band, 8);
-    band = std::min<int64_t>(band, 4096);
+    band = std::max<int64_t>(band, 64);
+    band = std::min<int64_t>(band, 256);
     return (int)band;
 }
 
@@ -197,11 +225,12 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.width = ctx->width;
     p.wwords = ctx->wwords;
     p.rows = (int32_t)ctx->rows;
-    const int sw = gol::strip_words(ctx->vec, gens);
+    const int vec = lane_words(ctx, gens);
+    const int sw = gol::strip_words(vec, gens);
     p.strips = (int32_t)((ctx->wwords + sw - 1) / sw);
     int64_t maxlen = 0;
     for (int k = 0; k < n; ++k) maxlen = std::max<int64_t>(maxlen, hi[k] - lo[k]);
-    p.band = pick_band(ctx, maxlen, p.strips);
+    p.band = pick_band(ctx, maxlen, p.strips, gens);
     int maxbands = 0;
     for (int k = 0; k < 2; ++k) {
         if (k < n) {
@@ -227,7 +256,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, ctx->vec, gens, life, slots != nullptr, clipped, gx, n, ctx->compute));
+    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, gx, n, ctx->compute));
     if (ev) {
         HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
         ctx->prof_gens += (uint64_t)gens;
@@ -295,7 +324,7 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
 
 // Pass depth for the next `remaining` generations.
 int pass_depth(const gol_ctx* ctx, uint32_t remaining) {
-    int G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : 1;
+    int G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : kAutoGensPerPass;
     G = std::min<int>(G, gol::kMaxGensPerPass);
     G = std::min<int64_t>(G, remaining);
     if (sharded(ctx)) G = std::min<int64_t>(G, ctx->rows);  // halo rows are sent from the shard
@@ -417,7 +446,7 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     ctx->vis_w = c.vis_width > 0 ? c.vis_width : c.width - 1;
     ctx->vis_h = c.vis_height > 0 ? c.vis_height : c.height - 1;
     ctx->device = c.device;
-    ctx->vec = (wwords % 4 == 0 && wwords >= 256) ? 4 : (wwords % 2 == 0 && wwords >= 128) ? 2 : 1;
+    ctx->vec_fixed = 0;
 
     auto fail = [&](int rc) {
         std::string msg = ctx->err;
@@ -678,13 +707,19 @@ int gol_profile_reset(gol_ctx* ctx) {
     return GOL_OK;
 }
 
-int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass) {
+int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (band_rows < 0 || gens_per_pass < 0 || gens_per_pass > gol::kMaxGensPerPass)
         return set_err(ctx, GOL_EINVAL, "tuning out of range (band_rows >= 0, 0 <= gens_per_pass <= %d)",
                        gol::kMaxGensPerPass);
+    if (words_per_lane != 0 && words_per_lane != 1 && words_per_lane != 2 && words_per_lane != 4)
+        return set_err(ctx, GOL_EINVAL, "words_per_lane must be 0 (auto), 1, 2 or 4");
+    if (words_per_lane > 0 && ctx->wwords % words_per_lane != 0)
+        return set_err(ctx, GOL_EINVAL, "words_per_lane %d does not divide the %d words of a row", words_per_lane,
+                       ctx->wwords);
     ctx->band_rows = band_rows;
-    if (gens_per_pass > 0) ctx->gens_per_pass = gens_per_pass;
+    ctx->gens_per_pass = gens_per_pass;
+    ctx->vec_fixed = words_per_lane;
     return GOL_OK;
 }
 

@@ -11,7 +11,7 @@ constexpr int kWavesPerWG = 4;   // 256-thread workgroups
 constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line each)
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
-constexpr int kMaxGensPerPass = 4;  // temporal blocking depth supported by the kernels
+constexpr int kMaxGensPerPass = 8;  // temporal blocking depth supported by the kernels
 
 // Hash constants (DESIGN.md "State hash"; oracle/gol_oracle.c oracle_hash_packed).
 constexpr uint32_t kHashK1 = 0x9E3779B9u;

@@ -71,6 +71,10 @@ hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool h
         case 2: return launch_step_g2(p, vec, life, hash, clipped, grid_x, grid_y, stream);
         case 3: return launch_step_g3(p, vec, life, hash, clipped, grid_x, grid_y, stream);
         case 4: return launch_step_g4(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 5: return launch_step_g5(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 6: return launch_step_g6(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 7: return launch_step_g7(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 8: return launch_step_g8(p, vec, life, hash, clipped, grid_x, grid_y, stream);
         default: return hipErrorInvalidValue;
     }
 }

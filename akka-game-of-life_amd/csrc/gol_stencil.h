@@ -536,5 +536,9 @@ hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, int, int, hi
 hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
 
 }  // namespace gol

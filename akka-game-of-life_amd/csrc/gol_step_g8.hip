@@ -1,0 +1,12 @@
+// gol_step_g8.hip -- instantiates the 8-generation-per-pass step kernels
+// (one translation unit per pass depth so they compile in parallel).
+#include "gol_stencil.h"
+
+namespace gol {
+
+hipError_t launch_step_g8(const StepParams& p, int vec, bool life, bool hash, bool clipped, int gx, int gy,
+                          hipStream_t st) {
+    return dev::launch_gens<8>(p, vec, life, hash, clipped, gx, gy, st);
+}
+
+}  // namespace gol

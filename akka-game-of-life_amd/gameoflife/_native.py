@@ -84,7 +84,7 @@ _SIGNATURES = {
     "gol_profile_enable": (_c.c_int, [_vp, _c.c_int]),
     "gol_profile_read": (_c.c_int, [_vp, ctypes.POINTER(_c.c_double), _u64p, _u64p]),
     "gol_profile_reset": (_c.c_int, [_vp]),
-    "gol_set_tuning": (_c.c_int, [_vp, _c.c_int32, _c.c_int32]),
+    "gol_set_tuning": (_c.c_int, [_vp, _c.c_int32, _c.c_int32, _c.c_int32]),
     "gol_selftest": (_c.c_int, [_c.c_int, _u32p]),
 }
 

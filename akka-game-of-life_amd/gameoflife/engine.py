@@ -139,8 +139,10 @@ class GolEngine:
     def profile_reset(self) -> None:
         self._chk(N.lib.gol_profile_reset(self._h))
 
-    def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0) -> None:
-        self._chk(N.lib.gol_set_tuning(self._h, band_rows, gens_per_pass))
+    def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0, words_per_lane: int = 0) -> None:
+        """Performance knobs only (gol_set_tuning): rows per band, generations
+        per HBM pass (1..8), words per lane (1/2/4, 0 = auto)."""
+        self._chk(N.lib.gol_set_tuning(self._h, band_rows, gens_per_pass, words_per_lane))
 
 
 def selftest(device: int = 0) -> np.ndarray:

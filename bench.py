@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CELL_UPDATE = 0.25
-DEFAULT_GPP = 2  # generations per HBM pass (scripts/tune.py sweep; DESIGN.md "Measurement")
+DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's automatic choice (6, from scripts/tune.py)
 
 
 def parse():
@@ -154,14 +154,15 @@ def main():
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
     value = W * H * a.steps / dt / 1e9
-    # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a pass
-    G = a.gpp
+    # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
+    # pass; G = generations that launch advances (the library's choice when --gpp 0)
+    G = round(gcov / launches) if launches else (a.gpp or 1)
     cells = W * (rows if world == 1 else max(rows - 2 * G, 0))
     roof = roofline(kms, launches, gcov, cells)
-    key = f"{W}x{H}/N{world}/G{G}/band{a.band}"
+    key = f"{W}x{H}/N{world}/G{G}"
     if roof is not None:
-        roof["kernel"] = ("gol::dev::step_kernel<4,LIFE>" if G == 1
-                          else f"gol::dev::multistep_kernel<4,{G},LIFE>")
+        roof["kernel"] = ("gol::dev::step_kernel<VEC,LIFE>" if G == 1
+                          else f"gol::dev::multistep_kernel<VEC,{G},LIFE>")
         t = pmc_traffic(key)
         if t is not None:
             roof["traffic"] = t.get("hbm_bytes_per_launch")
@@ -193,13 +194,13 @@ def main():
         if not a.no_secondary:
             S = 65536
             with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
-                e2.set_tuning(band_rows=a.band, gens_per_pass=G)
+                e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
                 e2.seed(0x5EED)
                 n2 = max(a.steps, 24)
                 dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, a.warmup, a.hash)
                 r2 = roofline(kms2, l2, g2, S * S)
                 if r2 is not None:
-                    t = pmc_traffic(f"{S}x{S}/N1/G{G}/band{a.band}")
+                    t = pmc_traffic(f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
                     if t is not None:
                         r2["traffic"] = t.get("hbm_bytes_per_launch")
                         r2["traffic_source"] = t.get("source")

@@ -172,10 +172,14 @@ int gol_profile_enable(gol_ctx* ctx, int enable);
 int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* generations);
 int gol_profile_reset(gol_ctx* ctx);
 
-/* Tuning knobs: rows per band streamed by one wave (0 = automatic), and the
- * number of generations fused per HBM pass (temporal blocking, 1..4; 0 keeps
- * the current value; default 1).  Results do not depend on either. */
-int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass);
+/* Tuning knobs (results never depend on them); 0 selects the automatic
+ * choice, which is also the default of a new context:
+ *   band_rows       rows of output streamed by one wave;
+ *   gens_per_pass   generations fused per HBM pass (temporal blocking, 1..8;
+ *                   automatic: 6, fewer when fewer generations remain);
+ *   words_per_lane  32-bit words each lane owns per row (1, 2 or 4; must
+ *                   divide the words of a row). */
+int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane);
 
 /* Diagnostic: runs a one-wave kernel exercising the cross-lane primitives the
  * step kernel relies on (DPP wave shifts, v_alignbit, scalar loads) and

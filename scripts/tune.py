@@ -31,25 +31,30 @@ def main():
     bands = [int(b) for b in os.environ.get("BANDS", "0,16,32,64,128,256").split(",")]
     gpps = [int(g) for g in os.environ.get("GPPS", "1,2,3,4").split(",")]
     rounds = int(os.environ.get("ROUNDS", "3"))
+    vecs = [int(v) for v in os.environ.get("VECS", "4").split(",")]
+    hashes = os.environ.get("HASH", "1") == "1"
     for edge in edges:
         gens = 48 if edge <= 65536 else 12
         with GolEngine(edge, edge) as e:
             e.seed(0x5EED)
             e.step(3)
-            keys = [(g, b) for g in gpps for b in bands]
+            keys = [(v, g, b) for v in vecs for g in gpps for b in bands]
             res = {k: [] for k in keys}
             resh = {k: [] for k in keys}
             for _ in range(rounds):
-                for (g, b) in keys:
-                    e.set_tuning(band_rows=b, gens_per_pass=g)
-                    res[(g, b)].append(measure(e, gens))
-                    resh[(g, b)].append(measure(e, gens, hashes=True))
+                for key in keys:
+                    v, g, b = key
+                    e.set_tuning(band_rows=b, gens_per_pass=g, words_per_lane=v)
+                    res[key].append(measure(e, gens))
+                    if hashes:
+                        resh[key].append(measure(e, gens, hashes=True))
             bytes_per_gen = edge * edge * 0.25
-            for (g, b) in keys:
-                k = min(x[0] for x in res[(g, b)])
-                w = min(x[1] for x in res[(g, b)])
-                kh = min(x[0] for x in resh[(g, b)])
-                print(f"edge={edge} G={g} band={b:5d} kernel_ms/gen={k:.4f} wall_ms/gen={w:.4f} "
+            for key in keys:
+                v, g, b = key
+                k = min(x[0] for x in res[key])
+                w = min(x[1] for x in res[key])
+                kh = min(x[0] for x in resh[key]) if hashes else float("nan")
+                print(f"edge={edge} VEC={v} G={g} band={b:5d} kernel_ms/gen={k:.4f} wall_ms/gen={w:.4f} "
                       f"GCUPS={edge * edge / k / 1e6:9.1f} frac={bytes_per_gen / k / 1e6 / 8000:.3f} | "
                       f"hash: kernel_ms/gen={kh:.4f} frac={bytes_per_gen / kh / 1e6 / 8000:.3f}", flush=True)
 

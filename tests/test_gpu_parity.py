@@ -27,17 +27,18 @@ def rule_obj(rule):
     return Rule(rule[0], rule[1])
 
 
-GPP = [1, 2, 3, 4]  # generations fused per HBM pass (temporal blocking depth)
+GPP = [1, 2, 3, 4, 5, 8]  # generations fused per HBM pass (temporal blocking depth)
 
 
-def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0, gpp=1):
+def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0, gpp=1,
+              vec=0):
     topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
     if cells is not None:
         board = O.pack(cells)
     else:
         board = O.seed_packed(W, H, seed if seed is not None else 0x5EED)
     with engine(W, H, topology=topology, rule=rule_obj(rule)) as e:
-        e.set_tuning(band_rows=band, gens_per_pass=gpp)
+        e.set_tuning(band_rows=band, gens_per_pass=gpp, words_per_lane=vec)
         e.load(board)
         assert e.hash() == O.hash_packed(board, W)
         got = e.step(gens, hashes=True)
@@ -114,6 +115,26 @@ def test_torus_random_rules(gpu, seed, gpp):
 @pytest.mark.parametrize("name", list(RULES))
 def test_torus_named_rules(gpu, name, gpp):
     check_run(32 * 96, 31, 10, RULES[name], "torus", seed=3, gpp=gpp)
+
+
+@pytest.mark.parametrize("gpp", [1, 2, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("vec", [1, 2, 4])
+def test_words_per_lane(gpu, vec, gpp):
+    # every lane width at every depth, full and partial strips, torus and clipped
+    check_run(32 * 520, 37, 9, O.LIFE, "torus", seed=vec, gpp=gpp, vec=vec)
+    check_run(32 * 12, 29, 9, (0x0C8, 0x1A6), "torus", seed=vec, gpp=gpp, vec=vec)
+    rng = np.random.default_rng(vec * 10 + gpp)
+    cells = (rng.random((31, 32 * 132 - 9)) < 0.5).astype(np.uint8)
+    check_run(32 * 132 - 9, 31, 9, O.LIFE, "ref-clipped", cells=cells, gpp=gpp, vec=vec)
+
+
+def test_tuning_rejects_bad_values(gpu):
+    from gameoflife import _native as N
+    with engine(32 * 6, 8) as e:
+        for kw in [dict(gens_per_pass=9), dict(words_per_lane=3), dict(words_per_lane=4),
+                   dict(band_rows=-1)]:
+            with pytest.raises(N.GolError):
+                e.set_tuning(**kw)
 
 
 @pytest.mark.parametrize("gpp", GPP)
