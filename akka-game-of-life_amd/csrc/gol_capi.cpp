@@ -35,6 +35,14 @@ struct EventPair {
 
 }  // namespace
 
+// In-process shard group: shards in row order, linked into a ring (torus) or
+// a chain (clipped); each shard's comm stream pulls its neighbours' edge rows.
+struct gol_group {
+    std::vector<gol_ctx*> shards;
+    bool torus = true;
+    std::string err;
+};
+
 struct gol_ctx {
     // geometry
     int64_t width = 0, height = 0, row0 = 0, rows = 0;
@@ -60,6 +68,9 @@ struct gol_ctx {
     // RCCL
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
+    // in-process shard group (gol_group_*): halos by device-to-device copies
+    gol_group* group = nullptr;
+    int gindex = 0;
     // tuning
     int32_t band_rows = 0;                                   // 0: automatic
     int32_t gens_per_pass = 0;                               // temporal blocking depth (0: automatic)
@@ -106,7 +117,12 @@ int set_err(gol_ctx* ctx, int code, const char* fmt, ...) {
                            __FILE__, __LINE__);                                                     \
     } while (0)
 
-bool sharded(const gol_ctx* c) { return c->nccl != nullptr && c->nranks > 1; }
+int64_t group_min_rows(const gol_group* g);
+size_t group_size(const gol_group* g);
+
+bool sharded(const gol_ctx* c) {
+    return (c->nccl != nullptr && c->nranks > 1) || (c->group != nullptr && group_size(c->group) > 1);
+}
 
 int bind(gol_ctx* ctx) {
     HIP_CHECK(ctx, hipSetDevice(ctx->device));
@@ -264,8 +280,35 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     return GOL_OK;
 }
 
-// One pass of G generations (temporal blocking, G <= kMaxGensPerPass).
-// slots: the hash accumulators of these G generations (G * kHashGenStride), or null.
+// Kernels of one sharded pass: the interior rows [G, rows-G) first -- they
+// need no halo and overlap the exchange -- then, once every event in
+// `halo_ready` has fired, the two boundary row blocks.  A missing neighbour
+// (clipped board ends) reads dead rows: zero_row holds kMaxGensPerPass of
+// them at the halo pitch.
+int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
+                         const hipEvent_t* halo_ready, int nready) {
+    uint32_t* cur = ctx->plane[ctx->cur];
+    uint32_t* nxt = ctx->plane[ctx->cur ^ 1];
+    const int32_t rows = (int32_t)ctx->rows;
+    const int64_t pitch = ctx->pitch;
+    const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
+    const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
+    if (rows > 2 * G) {
+        const int32_t lo[1] = {G}, hi[1] = {rows - G};
+        int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
+        if (rc) return rc;
+        for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
+        const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
+        return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false);
+    }
+    for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
+    const int32_t lo[1] = {0}, hi[1] = {rows};
+    return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
+}
+
+// One pass of G generations (temporal blocking, G <= kMaxGensPerPass) of a
+// stand-alone or RCCL-sharded context.  slots: the hash accumulators of these
+// G generations (G * kHashGenStride), or null.
 int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
     uint32_t* cur = ctx->plane[ctx->cur];
     uint32_t* nxt = ctx->plane[ctx->cur ^ 1];
@@ -277,6 +320,8 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         const int32_t lo[1] = {0}, hi[1] = {rows};
         int rc = launch_ranges(ctx, G, cur, nxt, ctx->zero_row, ctx->zero_row, 0, torus, slots, 1, lo, hi, true);
         if (rc) return rc;
+    } else if (ctx->group) {
+        return set_err(ctx, GOL_ESTATE, "context belongs to a shard group: step it with gol_group_step");
     } else {
         const int up = (ctx->rank + ctx->nranks - 1) % ctx->nranks;
         const int down = (ctx->rank + 1) % ctx->nranks;
@@ -296,43 +341,109 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         if (has_up) NCCL_CHECK(ctx, ncclRecv(ctx->halo_top, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
         if (has_down) NCCL_CHECK(ctx, ncclRecv(ctx->halo_bot, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
         NCCL_CHECK(ctx, ncclGroupEnd());
+        // The event covers the sends too: the next pass overwrites this plane
+        // only after the boundary kernels, which wait for it.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
-        // A missing neighbour (clipped board ends) reads dead rows: zero_row
-        // holds kMaxGensPerPass of them at the same pitch as the halos.
-        const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
-        const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
-        if (rows > 2 * G) {
-            // interior rows overlap the exchange; boundary row blocks follow it
-            const int32_t lo[1] = {G}, hi[1] = {rows - G};
-            int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
-            if (rc) return rc;
-            HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
-            const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
-            rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false);
-            if (rc) return rc;
-        } else {
-            HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_halo, 0));
-            const int32_t lo[1] = {0}, hi[1] = {rows};
-            int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
-            if (rc) return rc;
-        }
+        int rc = sharded_pass_kernels(ctx, G, slots, has_up, has_down, &ctx->ev_halo, 1);
+        if (rc) return rc;
     }
     ctx->cur ^= 1;
     ctx->epoch += (uint64_t)G;
     return GOL_OK;
 }
 
-// Pass depth for the next `remaining` generations.
+size_t group_size(const gol_group* g) { return g->shards.size(); }
+
+int64_t group_min_rows(const gol_group* g) {
+    int64_t m = INT64_MAX;
+    for (const gol_ctx* s : g->shards) m = std::min(m, s->rows);
+    return m;
+}
+
+int group_fail(gol_group* g, const gol_ctx* s, int rc) {
+    g->err = "shard " + std::to_string(s->gindex) + ": " + s->err;
+    return rc;
+}
+
+// One pass of G generations over every shard of an in-process group.  Each
+// shard's comm stream pulls its neighbours' G edge rows into its halo
+// buffers (hipMemcpyPeerAsync: the shards may live on different GPUs); the
+// kernels then run exactly as in an RCCL-sharded pass.  Ordering:
+//  - a pull waits for the neighbour's plane to be final (its ev_ready);
+//  - a shard's boundary kernels wait for its own pulls and for its
+//    neighbours' pulls (ev_halo of all three), so its next pass cannot
+//    overwrite rows a neighbour is still reading, and its next pull cannot
+//    overwrite halo rows its boundary kernels still read.
+int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slots) {
+    const int n = (int)g->shards.size();
+    for (gol_ctx* s : g->shards) {
+        if (int rc = bind(s)) return group_fail(g, s, rc);
+        if (hipEventRecord(s->ev_ready, s->compute) != hipSuccess)
+            return group_fail(g, s, set_err(s, GOL_EHIP, "hipEventRecord failed"));
+    }
+    for (int k = 0; k < n; ++k) {
+        gol_ctx* s = g->shards[k];
+        gol_ctx* up = g->shards[(k + n - 1) % n];
+        gol_ctx* dn = g->shards[(k + 1) % n];
+        const bool has_up = g->torus || k > 0, has_down = g->torus || k < n - 1;
+        const size_t bytes = (size_t)G * s->pitch * sizeof(uint32_t);
+        if (int rc = bind(s)) return group_fail(g, s, rc);
+        hipError_t e = hipStreamWaitEvent(s->comm, s->ev_ready, 0);
+        if (e == hipSuccess && has_up) e = hipStreamWaitEvent(s->comm, up->ev_ready, 0);
+        if (e == hipSuccess && has_down) e = hipStreamWaitEvent(s->comm, dn->ev_ready, 0);
+        if (e == hipSuccess && has_up)
+            e = hipMemcpyPeerAsync(s->halo_top, s->device, up->plane[up->cur] + (up->rows - G) * up->pitch, up->device,
+                                   bytes, s->comm);
+        if (e == hipSuccess && has_down)
+            e = hipMemcpyPeerAsync(s->halo_bot, s->device, dn->plane[dn->cur], dn->device, bytes, s->comm);
+        if (e == hipSuccess) e = hipEventRecord(s->ev_halo, s->comm);
+        if (e != hipSuccess)
+            return group_fail(g, s, set_err(s, GOL_EHIP, "halo pull failed: %s", hipGetErrorString(e)));
+    }
+    for (int k = 0; k < n; ++k) {
+        gol_ctx* s = g->shards[k];
+        gol_ctx* up = g->shards[(k + n - 1) % n];
+        gol_ctx* dn = g->shards[(k + 1) % n];
+        const bool has_up = g->torus || k > 0, has_down = g->torus || k < n - 1;
+        hipEvent_t ready[3];
+        int nr = 0;
+        ready[nr++] = s->ev_halo;
+        if (has_up) ready[nr++] = up->ev_halo;
+        if (has_down) ready[nr++] = dn->ev_halo;
+        if (int rc = bind(s)) return group_fail(g, s, rc);
+        if (int rc = sharded_pass_kernels(s, G, slots.empty() ? nullptr : slots[k], has_up, has_down, ready, nr))
+            return group_fail(g, s, rc);
+    }
+    for (gol_ctx* s : g->shards) {
+        s->cur ^= 1;
+        s->epoch += (uint64_t)G;
+    }
+    return GOL_OK;
+}
+
+// Pass depth for the next `remaining` generations.  Every shard of a ring
+// must pick the same G (their halo messages must match), so a sharded pass
+// is capped by the smallest shard of the decomposition, floor(H / N).
 int pass_depth(const gol_ctx* ctx, uint32_t remaining) {
     int G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : kAutoGensPerPass;
     G = std::min<int>(G, gol::kMaxGensPerPass);
     G = std::min<int64_t>(G, remaining);
-    if (sharded(ctx)) G = std::min<int64_t>(G, ctx->rows);  // halo rows are sent from the shard
+    if (ctx->nccl && ctx->nranks > 1) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
+    if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return std::max(G, 1);
 }
 
 void destroy_impl(gol_ctx* c) {
     if (!c) return;
+    if (c->group) {
+        // a lost shard (the analogue of DeathWatch's Terminated, BoardCreator.scala:120-121):
+        // the group keeps a hole and refuses to step until it is rebuilt
+        gol_group* g = c->group;
+        for (auto& s : g->shards)
+            if (s == c) s = nullptr;
+        g->err = "shard " + std::to_string(c->gindex) + " was destroyed; rebuild the group";
+        c->group = nullptr;
+    }
     hipSetDevice(c->device);
     if (c->compute) hipStreamSynchronize(c->compute);
     if (c->comm) hipStreamSynchronize(c->comm);
@@ -742,6 +853,125 @@ int gol_selftest(int device, uint32_t* report) {
     hipFree(d_in);
     hipFree(d_out);
     return GOL_OK;
+}
+
+int gol_group_create(gol_group** out, gol_ctx* const* shards, int n) {
+    if (!out || !shards || n < 1) return set_err(nullptr, GOL_EINVAL, "gol_group_create: bad arguments");
+    *out = nullptr;
+    const gol_ctx* a = shards[0];
+    int64_t next_row = 0;
+    for (int k = 0; k < n; ++k) {
+        const gol_ctx* s = shards[k];
+        if (!s) return set_err(nullptr, GOL_EINVAL, "shard %d is null", k);
+        if (s->group || s->nccl)
+            return set_err(nullptr, GOL_ESTATE, "shard %d already belongs to a group or an RCCL ring", k);
+        if (s->width != a->width || s->height != a->height || s->topology != a->topology ||
+            s->birth != a->birth || s->survive != a->survive || s->vis_w != a->vis_w || s->vis_h != a->vis_h)
+            return set_err(nullptr, GOL_EINVAL, "shard %d: board geometry or rule differs from shard 0", k);
+        if (s->epoch != a->epoch) return set_err(nullptr, GOL_ESTATE, "shard %d is at a different epoch", k);
+        if (s->row0 != next_row)
+            return set_err(nullptr, GOL_EINVAL, "shard %d starts at row %lld, expected %lld (row order, no gaps)", k,
+                           (long long)s->row0, (long long)next_row);
+        next_row += s->rows;
+    }
+    if (next_row != a->height)
+        return set_err(nullptr, GOL_EINVAL, "shards cover %lld of %lld rows", (long long)next_row,
+                       (long long)a->height);
+    gol_group* g = new gol_group();
+    g->torus = a->topology == GOL_TORUS;
+    for (int k = 0; k < n; ++k) {
+        g->shards.push_back(shards[k]);
+        shards[k]->group = g;
+        shards[k]->gindex = k;
+    }
+    // peer access between neighbouring shards on different GPUs (best effort:
+    // hipMemcpyPeerAsync falls back to staging without it)
+    for (int k = 0; k < n; ++k) {
+        gol_ctx* s = g->shards[k];
+        gol_ctx* dn = g->shards[(k + 1) % n];
+        if (s->device != dn->device) {
+            int ok = 0;
+            if (hipDeviceCanAccessPeer(&ok, s->device, dn->device) == hipSuccess && ok) {
+                hipSetDevice(s->device);
+                (void)hipDeviceEnablePeerAccess(dn->device, 0);
+                hipSetDevice(dn->device);
+                (void)hipDeviceEnablePeerAccess(s->device, 0);
+            }
+        }
+    }
+    (void)hipGetLastError();  // clear "peer access already enabled"
+    *out = g;
+    return GOL_OK;
+}
+
+const char* gol_group_last_error(const gol_group* g) { return g ? g->err.c_str() : ""; }
+
+int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
+    if (!g) return set_err(nullptr, GOL_EINVAL, "null group");
+    for (const gol_ctx* s : g->shards)
+        if (!s) return GOL_ESTATE;  // g->err names the lost shard
+    if (generations == 0) return GOL_OK;
+    const size_t per = (size_t)gol::kHashGenStride;
+    const int n = (int)g->shards.size();
+    constexpr uint32_t kChunk = 1024;
+    std::vector<uint64_t> part;
+    for (uint32_t g0 = 0; g0 < generations; g0 += kChunk) {
+        const uint32_t cnt = std::min(kChunk, generations - g0);
+        std::vector<unsigned long long*> base;
+        if (hashes_out) {
+            for (gol_ctx* s : g->shards) {
+                if (int rc = bind(s)) return group_fail(g, s, rc);
+                if (int rc = ensure_slots(s, cnt)) return group_fail(g, s, rc);
+                if (hipMemsetAsync(s->slots, 0, cnt * per * sizeof(unsigned long long), s->compute) != hipSuccess)
+                    return group_fail(g, s, set_err(s, GOL_EHIP, "hipMemsetAsync failed"));
+                base.push_back(s->slots);
+            }
+        }
+        for (uint32_t done = 0; done < cnt;) {
+            const int G = pass_depth(g->shards[0], cnt - done);
+            std::vector<unsigned long long*> slots;
+            for (unsigned long long* b : base) slots.push_back(b + done * per);
+            if (int rc = group_pass(g, G, slots)) return rc;
+            done += (uint32_t)G;
+        }
+        if (hashes_out) {
+            for (uint32_t k = 0; k < cnt; ++k) hashes_out[g0 + k] = 0;
+            part.resize(cnt);
+            for (int k = 0; k < n; ++k) {
+                gol_ctx* s = g->shards[k];
+                if (int rc = bind(s)) return group_fail(g, s, rc);
+                if (hipMemcpyAsync(s->host_slots.data(), s->slots, cnt * per * sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, s->compute) != hipSuccess ||
+                    hipStreamSynchronize(s->compute) != hipSuccess)
+                    return group_fail(g, s, set_err(s, GOL_EHIP, "hash readback failed"));
+                fold_slots(s, cnt, part.data());
+                for (uint32_t j = 0; j < cnt; ++j) hashes_out[g0 + j] += part[j];
+            }
+        }
+    }
+    return GOL_OK;
+}
+
+int gol_group_sync(gol_group* g) {
+    if (!g) return set_err(nullptr, GOL_EINVAL, "null group");
+    for (gol_ctx* s : g->shards) {
+        if (!s) continue;
+        if (int rc = gol_sync(s)) return group_fail(g, s, rc);
+    }
+    return GOL_OK;
+}
+
+void gol_group_destroy(gol_group* g) {
+    if (!g) return;
+    for (gol_ctx* s : g->shards) {
+        if (!s) continue;
+        hipSetDevice(s->device);
+        hipStreamSynchronize(s->comm);
+        hipStreamSynchronize(s->compute);
+        s->group = nullptr;
+        s->gindex = 0;
+    }
+    delete g;
 }
 
 }  // extern "C"

@@ -145,6 +145,59 @@ class GolEngine:
         self._chk(N.lib.gol_set_tuning(self._h, band_rows, gens_per_pass, words_per_lane))
 
 
+class ShardGroup:
+    """In-process group of shard engines of one board (gol_group_*): stepped
+    in lockstep with device-to-device halo copies.  Engines must be given in
+    row order and cover the board; they stay owned by the caller."""
+
+    def __init__(self, shards: list[GolEngine]):
+        self.shards = list(shards)
+        arr = (ctypes.c_void_p * len(shards))(*[s._h.value for s in shards])
+        h = ctypes.c_void_p()
+        N.check(N.lib.gol_group_create(ctypes.byref(h), arr, len(shards)))
+        self._h = h
+
+    def _chk(self, rc: int) -> None:
+        if rc != N.GOL_OK:
+            raise N.GolError(rc, (N.lib.gol_group_last_error(self._h) or b"").decode())
+
+    def step(self, generations: int = 1, hashes: bool = False):
+        """Advance every shard; returns the global per-generation hashes if asked."""
+        if hashes:
+            out = np.zeros(generations, dtype=np.uint64)
+            self._chk(N.lib.gol_group_step(self._h, generations, out.ctypes.data_as(N._u64p)))
+            return out
+        self._chk(N.lib.gol_group_step(self._h, generations, None))
+        return None
+
+    def sync(self) -> None:
+        self._chk(N.lib.gol_group_sync(self._h))
+
+    @property
+    def epoch(self) -> int:
+        return self.shards[0].epoch
+
+    def snapshot(self) -> np.ndarray:
+        return np.vstack([s.snapshot() for s in self.shards])
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            N.lib.gol_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def selftest(device: int = 0) -> np.ndarray:
     rep = np.zeros(256, dtype=np.uint32)
     N.check(N.lib.gol_selftest(device, rep.ctypes.data_as(N._u32p)))

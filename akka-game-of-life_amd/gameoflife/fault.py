@@ -1,0 +1,140 @@
+"""Fault path: periodic shard checkpoints, shard loss and re-spawn.
+
+Reference behaviour:
+* a cell actor dies (node loss, or an injected ``DoCrashMsg``,
+  ``BoardCreator.scala:97-102``, ``CellActor.scala:53-55,95-96``);
+* ``BoardCreator.onCellTermination`` re-deploys it at the same position on a
+  random surviving node with its epoch-0 state and re-wires the neighbour
+  refs (``BoardCreator.scala:138-154``);
+* the new cell replays epochs 1..step from its neighbours' never-pruned
+  histories (``CellActor.scala:34,71-74,86``).
+
+Here a shard (a row block in HBM) is the unit that dies.  Every
+``checkpoint_every`` generations all shards save a consistent checkpoint
+(``gol_checkpoint``: epoch + packed rows) to host memory (optionally also to
+files).  When a shard is lost the group is rebuilt with a new context for the
+dead rows -- on any surviving GPU, possibly next to a shard it already hosts
+-- every shard rolls back to the last checkpoint (global rollback; the
+counter-based board seed also allows regenerating epoch 0 as the reference
+does), and the lost generations are replayed.  Generations are a pure
+function of the checkpoint, so the per-generation hashes equal those of an
+uninterrupted run.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from .engine import GolEngine, ShardGroup
+from .shard import shard_rows_py
+
+
+class ShardedSimulation:
+    def __init__(self, width: int, height: int, nshards: int, devices: list[int] | None = None,
+                 topology: str = "torus", rule="life", seed: int = 0x5EED,
+                 checkpoint_every: int = 10, checkpoint_dir: str | None = None,
+                 gens_per_pass: int = 0):
+        self.width, self.height, self.n = width, height, nshards
+        self.devices = list(devices) if devices else [0]
+        self.topology, self.rule = topology, rule
+        self.checkpoint_every = checkpoint_every
+        self.checkpoint_dir = checkpoint_dir
+        self.gens_per_pass = gens_per_pass
+        self.placement = [self.devices[k % len(self.devices)] for k in range(nshards)]
+        self.shards: list[GolEngine | None] = [self._make(k, self.placement[k]) for k in range(nshards)]
+        for s in self.shards:
+            s.seed(seed)
+        self.group: ShardGroup | None = ShardGroup(self.shards)
+        self.hashes: list[int] = []          # global per-generation hashes, epochs 1..epoch
+        self.epoch = 0
+        self.ckpt_epoch = -1
+        self.ckpt: list[bytes] = []
+        self.events: list[str] = []
+        self.checkpoint()
+
+    def _make(self, k: int, device: int) -> GolEngine:
+        row0, rows = shard_rows_py(self.height, k, self.n)
+        e = GolEngine(self.width, self.height, topology=self.topology, rule=self.rule, device=device,
+                      row0=row0, rows=rows)
+        e.set_tuning(gens_per_pass=self.gens_per_pass)
+        return e
+
+    # ----------------------------------------------------------- checkpoints
+    def checkpoint(self) -> None:
+        self.ckpt = [s.checkpoint() for s in self.shards]
+        self.ckpt_epoch = self.epoch
+        if self.checkpoint_dir:
+            os.makedirs(self.checkpoint_dir, exist_ok=True)
+            for k, blob in enumerate(self.ckpt):
+                tmp = os.path.join(self.checkpoint_dir, f"shard{k}.ckpt.tmp")
+                with open(tmp, "wb") as f:
+                    f.write(blob)
+                os.replace(tmp, os.path.join(self.checkpoint_dir, f"shard{k}.ckpt"))
+        self.events.append(f"checkpoint@{self.epoch}")
+
+    # ------------------------------------------------------------------ run
+    def step(self, generations: int) -> list[int]:
+        """Advance, checkpointing at every multiple of checkpoint_every."""
+        if self.group is None:
+            raise RuntimeError("a shard is lost: respawn() before stepping")
+        out: list[int] = []
+        while generations > 0:
+            k = self.checkpoint_every
+            to_ckpt = (k - self.epoch % k) if k else generations
+            n = min(generations, to_ckpt)
+            hs = [int(h) for h in self.group.step(n, hashes=True)]
+            self.epoch += n
+            self.hashes.extend(hs)
+            out.extend(hs)
+            generations -= n
+            if k and self.epoch % k == 0:
+                self.checkpoint()
+        return out
+
+    # ---------------------------------------------------------------- faults
+    def kill(self, k: int) -> None:
+        """Lose shard k (its context and device memory are gone)."""
+        self.shards[k].close()            # the group now has a hole (gol_group_step -> GOL_ESTATE)
+        self.shards[k] = None
+        self.group.close()
+        self.group = None
+        self.events.append(f"kill shard {k} @{self.epoch}")
+
+    def respawn(self, k: int, device: int | None = None) -> list[int]:
+        """Re-spawn shard k on `device` (default: the next surviving device),
+        roll every shard back to the last checkpoint and replay to the epoch
+        reached before the failure.  Returns the replayed hashes."""
+        if device is None:
+            alive = [d for d in self.devices if d != self.placement[k]] or self.devices
+            device = alive[0]
+        self.placement[k] = device
+        self.shards[k] = self._make(k, device)
+        blobs = self.ckpt
+        if self.checkpoint_dir:  # survive the loss of host memory too
+            blobs = []
+            for j in range(self.n):
+                with open(os.path.join(self.checkpoint_dir, f"shard{j}.ckpt"), "rb") as f:
+                    blobs.append(f.read())
+        for s, blob in zip(self.shards, blobs):
+            s.restore(blob)
+        target = self.epoch
+        self.epoch = self.ckpt_epoch
+        lost = self.hashes[self.ckpt_epoch:]
+        del self.hashes[self.ckpt_epoch:]
+        self.group = ShardGroup(self.shards)
+        self.events.append(f"respawn shard {k} on device {device}, rollback to {self.ckpt_epoch}")
+        replayed = self.step(target - self.epoch) if target > self.epoch else []
+        if replayed != lost:
+            raise AssertionError("replayed generations differ from the lost ones")
+        return replayed
+
+    def snapshot(self) -> np.ndarray:
+        return np.vstack([s.snapshot() for s in self.shards])
+
+    def close(self) -> None:
+        if self.group is not None:
+            self.group.close()
+        for s in self.shards:
+            if s is not None:
+                s.close()

@@ -163,6 +163,22 @@ int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank,
  * place (the per-generation hash reduction). */
 int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count);
 
+/* In-process shard group: several shard contexts of one board, in row order
+ * and covering it without gaps, possibly on different GPUs (or several on
+ * one), stepped in lockstep with halo rows pulled by device-to-device copies
+ * (the same interior / boundary schedule as an RCCL ring).  This is how one
+ * surviving GPU hosts a re-spawned shard next to its own (the reference
+ * re-deploys a dead cell on a random surviving node, BoardCreator.scala:138-154).
+ * Destroying a member leaves a hole: gol_group_step then fails with
+ * GOL_ESTATE until the group is rebuilt.  gol_group_destroy unlinks the
+ * shards without destroying them.  hashes_out receives the global hash. */
+typedef struct gol_group gol_group;
+int gol_group_create(gol_group** out, gol_ctx* const* shards, int n);
+int gol_group_step(gol_group* group, uint32_t generations, uint64_t* hashes_out);
+int gol_group_sync(gol_group* group);
+const char* gol_group_last_error(const gol_group* group);
+void gol_group_destroy(gol_group* group);
+
 /* Kernel timing: when enabled, the dominant step-kernel launch of every pass
  * (the whole shard, or a sharded shard's interior rows) is bracketed by HIP
  * events on the stream it runs on.  gol_profile_read returns, since the last

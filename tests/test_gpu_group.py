@@ -1,0 +1,111 @@
+"""GPU: the sharded schedule (interior rows || halo exchange, then boundary
+rows; G-deep halos) through an in-process shard group, and the fault path
+(BASELINE.json config 5: kill a shard mid-run, re-spawn it from the last
+checkpoint, hashes unchanged).  Bit-exact against the CPU oracle."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def make_group(W, H, n, topology="torus", rule="life", gpp=0, seed=77, cells=None):
+    from gameoflife.engine import GolEngine, ShardGroup
+    from gameoflife.shard import shard_rows_py
+    shards = []
+    full = O.pack(cells) if cells is not None else O.seed_packed(W, H, seed)
+    for k in range(n):
+        r0, rows = shard_rows_py(H, k, n)
+        e = GolEngine(W, H, topology=topology, rule=rule, row0=r0, rows=rows)
+        e.set_tuning(gens_per_pass=gpp)
+        e.load(full[r0:r0 + rows])
+        shards.append(e)
+    return shards, ShardGroup(shards), full
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("gpp", [1, 2, 6])
+def test_group_torus_matches_oracle(gpu, n, gpp):
+    W, H, gens = 32 * 300, 83, 13  # uneven shards (83 rows over n), rows <= 2G for some
+    shards, g, full = make_group(W, H, n, gpp=gpp)
+    got = g.step(gens, hashes=True)
+    board = g.snapshot()
+    ref, want = O.run_packed(full, W, gens, O.TORUS, O.LIFE)
+    np.testing.assert_array_equal(got, want)
+    assert (board == ref).all()
+    g.close()
+    for s in shards:
+        s.close()
+
+
+@pytest.mark.parametrize("n", [2, 4])
+@pytest.mark.parametrize("gpp", [1, 3, 6])
+def test_group_clipped_matches_oracle(gpu, n, gpp):
+    W, H, gens = 1000, 61, 9
+    rng = np.random.default_rng(n * 10 + gpp)
+    cells = (rng.random((H, W)) < 0.5).astype(np.uint8)
+    shards, g, full = make_group(W, H, n, topology="ref-clipped", rule="B36/S23", gpp=gpp, cells=cells)
+    got = g.step(gens, hashes=True)
+    board = g.snapshot()
+    ref, want = O.run_packed(full, W, gens, O.REF_CLIPPED, (0x48, 0x0C))
+    np.testing.assert_array_equal(got, want)
+    assert (board == ref).all()
+    g.close()
+    for s in shards:
+        s.close()
+
+
+def test_group_rejects_bad_layout_and_lost_shard(gpu):
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine, ShardGroup
+    a = GolEngine(256, 40, row0=0, rows=20)
+    b = GolEngine(256, 40, row0=21, rows=19)  # gap at row 20
+    with pytest.raises(N.GolError):
+        ShardGroup([a, b])
+    b.close()
+    b = GolEngine(256, 40, row0=20, rows=20)
+    g = ShardGroup([a, b])
+    g.step(3)
+    b.close()  # the shard dies: the group has a hole
+    with pytest.raises(N.GolError) as ei:
+        g.step(1)
+    assert ei.value.code == N.GOL_ESTATE and "destroyed" in ei.value.message
+    g.close()
+    a.close()
+
+
+@pytest.mark.parametrize("ckpt_dir", [False, True])
+def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir):
+    """BASELINE.json config 5 in miniature: 8 shards, checkpoint every 10,
+    shard 3 killed at generation 25 of 50, re-spawned next to a survivor,
+    rolled back and replayed: every per-generation hash equals the
+    uninterrupted run's, and the final board equals the oracle's."""
+    from gameoflife import _native as N
+    from gameoflife.fault import ShardedSimulation
+    W, H = 32 * 256, 1024
+    devices = list(range(N.device_count()))
+    ref = ShardedSimulation(W, H, 8, devices, checkpoint_every=10)
+    want = ref.step(50)
+    ref_board = ref.snapshot()
+    ref.close()
+
+    sim = ShardedSimulation(W, H, 8, devices, checkpoint_every=10,
+                            checkpoint_dir=str(tmp_path) if ckpt_dir else None)
+    got = sim.step(25)
+    sim.kill(3)
+    with pytest.raises(RuntimeError):
+        sim.step(1)
+    replayed = sim.respawn(3)
+    assert len(replayed) == 5 and sim.epoch == 25
+    got += sim.step(25)
+    assert got == want
+    assert sim.hashes == want
+    assert (sim.snapshot() == ref_board).all()
+    assert any(e.startswith("respawn shard 3") for e in sim.events)
+    sim.close()
+
+    board0 = O.seed_packed(W, H, 0x5EED)
+    final, oh = O.run_packed(board0, W, 50, O.TORUS, O.LIFE)
+    assert [int(x) for x in oh] == want
+    assert (final == ref_board).all()
