@@ -61,12 +61,13 @@ class LoggerActor:
     """LoggerActor.scala:30-46 output format.
 
     The reference prints, per epoch, ``At epoch:N``, a dash line of length
-    2x+1, y rows ``[a,b,...]`` of x cells each and a closing dash line.  It
-    fills the rows from CellStateMsgs in *arrival order* (:32-33 prepend, :17
-    slice) and prints when x*y messages (not (x+1)*(y+1)) have arrived
-    (:28,35), so its rows are not positional.  This port prints the board
-    positionally: row y lists cells x = 0..x-1 of the first x columns and y
-    rows, i.e. the same shape the reference prints.
+    2x+1, rows ``[a,b,...]`` and a closing dash line.  It fills the rows
+    from CellStateMsgs in *arrival order* (:32-33 prepend, :17 slice) and
+    prints once x*y of the (x+1)*(y+1) messages have arrived (:28,35), so
+    its rows are neither positional nor complete.  This port keeps the
+    format but prints the whole board positionally: one row per board row,
+    one entry per cell (the native frontend, csrc/gol_frontend.cpp, prints
+    the same text).
     """
 
     def __init__(self, board_size: BoardSize, sink: Callable[[str], None] | None = None):
@@ -75,14 +76,14 @@ class LoggerActor:
         self.sink = sink or self.lines.append
 
     @staticmethod
-    def format_epoch(cells: np.ndarray, epoch: int, board_size: BoardSize) -> list[str]:
-        x, y = board_size
-        rows = ["[" + ",".join(str(int(v)) for v in cells[r, :x]) + "]" for r in range(y)]
-        dash = "-" * (x * 2 + 1)
+    def format_epoch(cells: np.ndarray, epoch: int) -> list[str]:
+        h, w = cells.shape
+        rows = ["[" + ",".join(str(int(v)) for v in cells[r]) + "]" for r in range(h)]
+        dash = "-" * (w * 2 + 1)
         return [f"At epoch:{epoch}", dash, *rows, dash + "\n"]
 
     def log_board(self, cells: np.ndarray, epoch: int) -> None:
-        for line in self.format_epoch(cells, epoch, self.board_size):
+        for line in self.format_epoch(cells, epoch):
             self.sink(line)
 
 

@@ -40,8 +40,8 @@ def test_all_coordinates_inclusive():
 
 def test_logger_format():
     cells = np.array([[1, 0, 1], [0, 1, 0], [0, 0, 0]], dtype=np.uint8)
-    lines = B.LoggerActor.format_epoch(cells, 4, (2, 2))
-    assert lines == ["At epoch:4", "-----", "[1,0]", "[0,1]", "-----\n"]
+    lines = B.LoggerActor.format_epoch(cells, 4)
+    assert lines == ["At epoch:4", "-------", "[1,0,1]", "[0,1,0]", "[0,0,0]", "-------\n"]
 
 
 def test_config_keys_and_durations():
@@ -114,8 +114,8 @@ def test_board_creator_drives_backend_and_logs():
     bc.next_step(3)
     assert bc.step == 5
     # logged after ticks reaching epochs 1, 2 and 5 (one multi-generation tick)
-    assert logger.lines[0] == "At epoch:1" and len(logger.lines) == 3 * (6 + 3)
-    assert logger.lines[18] == "At epoch:5"
+    assert logger.lines[0] == "At epoch:1" and len(logger.lines) == 3 * (7 + 3)
+    assert logger.lines[20] == "At epoch:5"
     assert bc.send_me_my_neighbours((0, 0)) == [(0, 1), (1, 0), (1, 1)]
 
 

@@ -75,6 +75,17 @@ def test_no_cpu_fallback():
     assert b"no CPU fallback" in N.lib.gol_last_error(None)
 
 
+def test_native_frontend_links_c_abi_only():
+    exe = os.path.join(ROOT, "akka-game-of-life_amd", "bin", "gol_frontend")
+    assert os.path.exists(exe)
+    # built with g++ against include/gol.h: no HIP runtime symbols referenced directly
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True).stdout
+    assert "gol_create" in syms and "hipMalloc" not in syms
+    if N.device_count() == 0:
+        p = subprocess.run([exe, "generations=1", "log.file=-"], capture_output=True, text=True)
+        assert p.returncode == 1 and "no HIP device" in p.stderr
+
+
 def test_create_validates_geometry():
     from gameoflife.engine import GolEngine
     for kw in [dict(width=33, height=8),                       # torus needs width % 32 == 0
