@@ -35,12 +35,13 @@ DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's automatic choice (6, f
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults are whole 6-generation passes (the automatic pass depth)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
     ap.add_argument("--band", type=int, default=0, help="rows per band (0 = auto)")
     ap.add_argument("--gpp", type=int, default=DEFAULT_GPP,
-                    help="generations fused per HBM pass (temporal blocking depth, 1..4)")
+                    help="generations fused per HBM pass (temporal blocking depth 1..8; 0 = automatic)")
     ap.add_argument("--hash", action="store_true", help="fuse the per-generation state hash")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")

@@ -1,0 +1,76 @@
+"""GPU: the RCCL-sharded path (gol_comm_init + G-deep halo send/recv) with
+2 and 3 ranks, one process each, all on the box's GPU(s).  If RCCL refuses
+several ranks on one GPU (duplicate-GPU check) and the box has fewer GPUs
+than ranks, the test is skipped with RCCL's message -- the driver's
+multi-GPU bench then exercises the path."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+W, H, GENS = 32 * 300, 96, 14
+
+
+def _worker(rank, world, uid_q, out_q, topology, gpp):
+    try:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        from gameoflife import _native as N
+        from gameoflife.engine import GolEngine
+        ndev = N.device_count()
+        row0, rows = N.shard_rows(H, rank, world)
+        e = GolEngine(W, H, topology=topology, rule="life", device=rank % ndev, row0=row0, rows=rows)
+        e.set_tuning(gens_per_pass=gpp)
+        full = O.seed_packed(W, H, 99)
+        e.load(full[row0:row0 + rows])
+        if rank == 0:
+            uid = N.unique_id()
+            for _ in range(world - 1):
+                uid_q.put(uid)
+        else:
+            uid = uid_q.get(timeout=60)
+        e.comm_init(uid, rank, world)
+        part = e.step(GENS, hashes=True)
+        total = e.allreduce_u64(part)
+        out_q.put((rank, row0, e.snapshot(), total.tolist(), None))
+        e.close()
+    except Exception as exc:  # report instead of hanging the parent
+        out_q.put((rank, None, None, None, f"{type(exc).__name__}: {exc}"))
+
+
+@pytest.mark.parametrize("world,topology,gpp", [(2, "torus", 1), (2, "torus", 6), (3, "torus", 4),
+                                                (2, "ref-clipped", 3)])
+def test_rccl_ring_matches_oracle(gpu, world, topology, gpp):
+    ctx = mp.get_context("spawn")
+    uid_q, out_q = ctx.Queue(), ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, uid_q, out_q, topology, gpp)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in range(world):
+            res.append(out_q.get(timeout=180))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [r[4] for r in res if r[4]]
+    if errs:
+        from gameoflife import _native as N
+        if N.device_count() < world and any("duplicate" in e.lower() or "rccl" in e.lower()
+                                            or "ncclInvalidUsage" in e for e in errs):
+            pytest.skip(f"RCCL cannot place {world} ranks on {N.device_count()} GPU(s): {errs[0]}")
+        raise AssertionError(errs)
+    res.sort()
+    board = np.vstack([r[2] for r in res])
+    topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
+    ref, want = O.run_packed(O.seed_packed(W, H, 99), W, GENS, topo, O.LIFE)
+    for r in res:
+        assert r[3] == [int(x) for x in want]
+    assert (board == ref).all()
