@@ -184,6 +184,18 @@ EventPair* next_event_pair(gol_ctx* ctx) {
 // results never depend on these choices.
 constexpr int kAutoGensPerPass = 6;  // best depth at 65536^2 and 262144^2
 
+// Multi-generation kernel formulation (gol_stencil.h): 1 = vertical-first,
+// 2 = horizontal-first (default: ~13.5 instead of ~15.4 VALU per word and
+// generation; +9 % at 262144^2, +24 % at 65536^2, profiles/r01_variant_ab.txt).
+// GOL_STENCIL_VARIANT overrides (A/B experiments).
+int stencil_variant() {
+    static const int v = [] {
+        const char* e = getenv("GOL_STENCIL_VARIANT");
+        return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 2;
+    }();
+    return v;
+}
+
 // Words per lane for a single-generation pass: 16-byte lane loads where the
 // row fills whole waves of them.
 int default_vec(int64_t wwords) {
@@ -202,6 +214,9 @@ int lane_words(const gol_ctx* ctx, int gens) {
         return (double)(w / v) / (double)(strips * 64);
     };
     const bool ok4 = w % 4 == 0 && w >= 4 * 62, ok2 = w % 2 == 0 && w >= 2 * 62;
+    // the horizontal-first kernel keeps 3 planes per ring row: 8-byte lanes
+    // (95 VGPRs at G = 6, 5 waves/SIMD) beat 16-byte lanes (183 VGPRs, 2 waves)
+    if (stencil_variant() == 2) return ok2 ? 2 : 1;
     if (ok4 && (!ok2 || util(4) >= util(2) - 0.03)) return 4;
     if (ok2) return 2;
     return 1;
@@ -262,6 +277,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
     p.birth = ctx->birth;
     p.survive = ctx->survive;
+    p.variant = stencil_variant();
     const bool clipped = ctx->topology == GOL_REF_CLIPPED;
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int64_t waves = (int64_t)p.strips * maxbands;

@@ -43,6 +43,7 @@ struct StepParams {
     int64_t halo_stride;       // words between halo rows (0: one row repeated)
     uint32_t birth;
     uint32_t survive;
+    int32_t variant;           // multi-generation kernel: 1 vertical-first, 2 horizontal-first
 };
 
 // Strip geometry of a launch: words covered per wave.

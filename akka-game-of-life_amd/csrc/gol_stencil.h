@@ -491,10 +491,197 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
     }
 }
 
+// --------------------------------------------------------------------------
+// G generations per pass, horizontal-first count (variant 2).
+//
+// On arrival every row r (input or stage output) gets its horizontal 3-sum
+// h = W(r) + r + E(r) (2 v_alignbit + 2 v_bitop3, 2 DPP moves per lane),
+// shared by the three output rows that read it.  Output row m then needs
+//   g(m) = h(m) - r(m)                 (the centre-less pair W + E, 2 ops)
+//   n = h(m-1) + h(m+1) + g(m)         (one carry-save layer, 4 ops)
+//   rule                               (2 ops for B3/S23)
+// ~12 + 2/VEC VALU per word-generation instead of ~15.  Each ring row keeps
+// (h0, h1, r) -- three planes -- so the rings hold more registers.
+// --------------------------------------------------------------------------
+constexpr uint32_t kAndOrNotC = 0xD0;  // a & (b | ~c)
+
+template <int VEC, bool CLIPPED>
+struct HRow {
+    uint32_t h0[VEC], h1[VEC], r[VEC];  // r: the visible row
+    uint32_t a[CLIPPED ? VEC : 1];       // clipped: the real row (alive bits)
+};
+
+template <int VEC, bool CLIPPED>
+__device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const uint32_t (&cmask)[VEC],
+                                       HRow<VEC, CLIPPED>& o) {
+    uint32_t rv[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        rv[j] = CLIPPED ? (vis ? (raw.w[j] & cmask[j]) : 0u) : raw.w[j];
+        if constexpr (CLIPPED) o.a[j] = raw.w[j];
+    }
+    const uint32_t left = dpp_shr1_zero(rv[VEC - 1]);  // halo lanes read zeros at the wave's ends
+    const uint32_t right = dpp_shl1_zero(rv[0]);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t w = __builtin_amdgcn_alignbit(rv[j], j == 0 ? left : rv[j - 1], 31);
+        const uint32_t e = __builtin_amdgcn_alignbit(j == VEC - 1 ? right : rv[j + 1], rv[j], 1);
+        o.h0[j] = GOL_BITOP3(w, rv[j], e, kXor3);
+        o.h1[j] = GOL_BITOP3(w, rv[j], e, kMaj);
+        o.r[j] = rv[j];
+    }
+}
+
+template <int VEC, bool LIFE, bool CLIPPED>
+__device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLIPPED>& A,
+                                        const HRow<VEC, CLIPPED>& C, const HRow<VEC, CLIPPED>& B,
+                                        const uint32_t (&omask)[VEC], Words<VEC>& out) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t g0 = C.h0[j] ^ C.r[j];
+        const uint32_t g1 = GOL_BITOP3(C.h1[j], C.h0[j], C.r[j], kAndOrNotC);
+        const uint32_t nb0 = GOL_BITOP3(A.h0[j], B.h0[j], g0, kXor3);
+        const uint32_t c0 = GOL_BITOP3(A.h0[j], B.h0[j], g0, kMaj);
+        const uint32_t pp = GOL_BITOP3(A.h1[j], B.h1[j], g1, kXor3);
+        const uint32_t qq = GOL_BITOP3(A.h1[j], B.h1[j], g1, kMaj);
+        const uint32_t al = CLIPPED ? C.a[j] : C.r[j];
+        uint32_t res;
+        if constexpr (LIFE) {
+            const uint32_t x = GOL_BITOP3(qq, pp, c0, kNotAXorBC);
+            res = GOL_BITOP3(x, nb0, al, kAAndBOrC);
+        } else {
+            const uint32_t n1b = pp ^ c0, k = pp & c0;
+            const uint32_t n2b = qq ^ k, n3b = qq & k;
+            uint32_t L[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) {
+                const uint32_t sm = ((p.survive >> q) & 1u) ? 0xFFFFFFFFu : 0u;
+                const uint32_t bm = ((p.birth >> q) & 1u) ? 0xFFFFFFFFu : 0u;
+                L[q] = bfi(al, sm, bm);
+            }
+            const uint32_t m01 = bfi(nb0, L[1], L[0]), m23 = bfi(nb0, L[3], L[2]);
+            const uint32_t m45 = bfi(nb0, L[5], L[4]), m67 = bfi(nb0, L[7], L[6]);
+            const uint32_t m03 = bfi(n1b, m23, m01), m47 = bfi(n1b, m67, m45);
+            const uint32_t m07 = bfi(n2b, m47, m03);
+            res = bfi(n3b, L[8], m07);
+        }
+        out.w[j] = CLIPPED ? (res & omask[j]) : res;
+    }
+}
+
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(const StepParams p) {
+    static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
+    static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
+    constexpr int kOut = (kWaveLanes - 2) * VEC;
+    const int lane = threadIdx.x & (kWaveLanes - 1);
+    const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
+    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
+    const int rg = blockIdx.y;
+    const int strip = wave % p.strips;
+    const int bandi = wave / p.strips;
+    unsigned long long acc[G];
+#pragma unroll
+    for (int s = 0; s < G; ++s) acc[s] = 0;
+
+    if (bandi < p.nbands[rg]) {
+        const int r_begin = p.row_lo[rg] + bandi * p.band;
+        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int nrows = r_end - r_begin;
+        const int n_in = nrows + 2 * G;
+        const int s0 = strip * kOut;
+        const int nout = min(kOut, p.wwords - s0);
+        const int col = s0 + (lane - 1) * VEC;
+        const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
+        int lcol;
+        bool incol;
+        if (p.wrap_x) {
+            lcol = col % p.wwords;
+            if (lcol < 0) lcol += p.wwords;
+            incol = true;
+        } else {
+            incol = col >= 0 && col < p.wwords;
+            lcol = incol ? col : 0;
+        }
+        uint32_t cmask[VEC], omask[VEC], lk1[VEC], lk2[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
+            omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
+            lk1[j] = (uint32_t)(col + j) * kHashK1;
+            lk2[j] = (uint32_t)(col + j) * kHashK2;
+        }
+        const bool up = (bandi & 1) != 0;
+        auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
+        auto vis = [&](int m) -> bool { return row_visible<CLIPPED>(p, brow(m)); };
+
+        Words<VEC> in[kMRing];
+        HRow<VEC, CLIPPED> hr[G][3];  // ring s: arrivals of stage-s rows (stage 0 = input), slot = row % 3
+#pragma unroll
+        for (int k = 0; k < kMRing; ++k)
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) in[k].w[j] = 0u;
+#pragma unroll
+        for (int s = 0; s < G; ++s)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    hr[s][k].h0[j] = hr[s][k].h1[j] = hr[s][k].r[j] = 0u;
+                    if constexpr (CLIPPED) hr[s][k].a[j] = 0u;
+                }
+
+        auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
+
+#pragma unroll
+        for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
+        for (int q0 = 0; q0 < n_in; q0 += kMRing) {
+#pragma unroll
+            for (int u = 0; u < kMRing; ++u) {
+                const int q = q0 + u;
+                load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
+                // input row q arrives at ring 0
+                arrive<VEC, CLIPPED>(in[u], vis(q), cmask, hr[0][u % 3]);
+#pragma unroll
+                for (int s = 1; s <= G; ++s) {
+                    // stage s: stream row m = q - s from ring s-1 rows m-1, m, m+1
+                    const int m = q - s;
+                    Words<VEC> o;
+                    rule_hg<VEC, LIFE, CLIPPED>(p, hr[s - 1][((u - s - 1) % 3 + 3) % 3],
+                                                hr[s - 1][((u - s) % 3 + 3) % 3],
+                                                hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
+                    const bool own_row = m >= G && m < n_in - G;
+                    if (s < G) {
+                        arrive<VEC, CLIPPED>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
+                        if constexpr (HASH) {
+                            if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                        }
+                    } else if (own_row) {
+                        const int r = brow(m);
+                        store_words<VEC>(p.nxt + (int64_t)r * p.pitch, lcol, owns, o);
+                        if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                    }
+                }
+            }
+        }
+        if (!owns) {
+#pragma unroll
+            for (int s = 0; s < G; ++s) acc[s] = 0;
+        }
+    }
+    if constexpr (HASH) {
+#pragma unroll
+        for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
+    }
+}
+
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     if constexpr (G == 1) {
         hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+    } else if (p.variant == 2) {
+        hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
     } else {
         hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
