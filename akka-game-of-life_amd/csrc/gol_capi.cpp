@@ -17,6 +17,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -81,6 +82,9 @@ struct gol_ctx {
     double prof_ms = 0.0;
     uint64_t prof_launches = 0;
     uint64_t prof_gens = 0;  // generations covered by the profiled launches
+    // occupancy
+    int num_cus = 0;
+    std::map<int, int64_t> occupancy_cache;
     std::string err;
 };
 
@@ -222,7 +226,8 @@ int lane_words(const gol_ctx* ctx, int gens) {
     return 1;
 }
 
-int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens) {
+// `resident`: waves the whole GPU holds at once for this kernel (0: unknown).
+int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t resident) {
     if (ctx->band_rows > 0) return ctx->band_rows;
     if (gens == 1) return 16;  // short bands: more waves in flight, seams hit the Infinity Cache
     // Multi-generation passes recompute 2G halo rows per band: keep bands
@@ -231,7 +236,46 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens) {
     int64_t band = (rows + bands - 1) / bands;
     band = std::max<int64_t>(band, 64);
     band = std::min<int64_t>(band, 256);
+    // Wave quantization on wide boards: when a pass is only a few rounds of
+    // resident waves, the last round is partly empty.  Model a pass as
+    // ceil(waves / resident) rounds of (band + 2G) stream rows and shrink the
+    // band (down to 60 %) when that fills the rounds better.  Measured on
+    // the N = 8 per-rank shape (262144 x 32768, 1.7 rounds at band 256):
+    // band 216 1.5-10 % faster on two boxes; with more rounds the effect is
+    // within box-to-box noise (profiles/r01_band_quantization.txt).  Narrow
+    // boards (< 32 strips) keep the plain choice (the model mispredicts 65536^2).
+    if (resident > 0 && strips >= 32) {
+        auto cost = [&](int64_t b) -> double {
+            const int64_t waves = (rows + b - 1) / b * strips;
+            return (double)((waves + resident - 1) / resident) * (double)(b + 2 * gens);
+        };
+        const int64_t full = (rows + band - 1) / band * strips;
+        if (full >= resident && full <= 3 * resident) {
+            int64_t best = band;
+            double best_cost = cost(band);
+            for (int64_t b = band - 1; b >= std::max<int64_t>(64, band * 6 / 10); --b) {
+                const double c = cost(b);
+                if (c < best_cost * 0.99) {
+                    best = b;
+                    best_cost = c;
+                }
+            }
+            band = best;
+        }
+    }
     return (int)band;
+}
+
+// Resident waves on the whole GPU for a launch (cached occupancy query).
+int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
+    const int key = ((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
+                    stencil_variant();
+    auto it = ctx->occupancy_cache.find(key);
+    if (it != ctx->occupancy_cache.end()) return it->second;
+    const int blocks = gol::resident_blocks_per_cu(vec, gens, stencil_variant(), life, hash, clipped);
+    const int64_t waves = (int64_t)blocks * gol::kWavesPerWG * ctx->num_cus;
+    ctx->occupancy_cache[key] = waves;
+    return waves;
 }
 
 // Launch one pass of `gens` generations over local row ranges [lo0,hi0)
@@ -261,7 +305,10 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.strips = (int32_t)((ctx->wwords + sw - 1) / sw);
     int64_t maxlen = 0;
     for (int k = 0; k < n; ++k) maxlen = std::max<int64_t>(maxlen, hi[k] - lo[k]);
-    p.band = pick_band(ctx, maxlen, p.strips, gens);
+    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
+    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
+    const int64_t resident = (n == 1 && gens > 1) ? resident_waves(ctx, vec, gens, life, slots != nullptr, clipped) : 0;
+    p.band = pick_band(ctx, maxlen, p.strips, gens, resident);
     int maxbands = 0;
     for (int k = 0; k < 2; ++k) {
         if (k < n) {
@@ -278,8 +325,6 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.birth = ctx->birth;
     p.survive = ctx->survive;
     p.variant = stencil_variant();
-    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
-    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int64_t waves = (int64_t)p.strips * maxbands;
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
@@ -574,6 +619,8 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     ctx->vis_h = c.vis_height > 0 ? c.vis_height : c.height - 1;
     ctx->device = c.device;
     ctx->vec_fixed = 0;
+    if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess)
+        ctx->num_cus = 0;
 
     auto fail = [&](int rc) {
         std::string msg = ctx->err;
@@ -847,6 +894,20 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     ctx->band_rows = band_rows;
     ctx->gens_per_pass = gens_per_pass;
     ctx->vec_fixed = words_per_lane;
+    return GOL_OK;
+}
+
+int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, int32_t* strip_words) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (gens_per_pass < 1 || gens_per_pass > gol::kMaxGensPerPass)
+        return set_err(ctx, GOL_EINVAL, "gens_per_pass out of range");
+    if (int rc = bind(ctx)) return rc;
+    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
+    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
+    const int vec = lane_words(ctx, gens_per_pass);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens_per_pass, stencil_variant(), life, false, clipped);
+    if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
+    if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
     return GOL_OK;
 }
 

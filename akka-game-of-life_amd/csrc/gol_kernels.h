@@ -55,6 +55,11 @@ int strip_words(int vec, int gens);
 hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped,
                        int grid_x, int grid_y, hipStream_t stream);
 
+// Resident 256-thread workgroups per CU of the step kernel instance a launch
+// with these parameters uses (hipOccupancyMaxActiveBlocksPerMultiprocessor);
+// 0 if unknown.
+int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped);
+
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width,
                        int64_t grow0, int32_t rows, uint64_t seed, hipStream_t stream);
 

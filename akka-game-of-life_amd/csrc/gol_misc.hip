@@ -79,6 +79,20 @@ hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool h
     }
 }
 
+int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped) {
+    switch (gens) {
+        case 1: return blocks_step_g1(vec, variant, life, hash, clipped);
+        case 2: return blocks_step_g2(vec, variant, life, hash, clipped);
+        case 3: return blocks_step_g3(vec, variant, life, hash, clipped);
+        case 4: return blocks_step_g4(vec, variant, life, hash, clipped);
+        case 5: return blocks_step_g5(vec, variant, life, hash, clipped);
+        case 6: return blocks_step_g6(vec, variant, life, hash, clipped);
+        case 7: return blocks_step_g7(vec, variant, life, hash, clipped);
+        case 8: return blocks_step_g8(vec, variant, life, hash, clipped);
+        default: return 0;
+    }
+}
+
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0, int32_t rows,
                        uint64_t seed, hipStream_t stream) {
     const int64_t total = (int64_t)rows * wwords;

@@ -690,6 +690,41 @@ hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     return hipGetLastError();
 }
 
+// Resident 256-thread workgroups per CU for a kernel instance (occupancy API).
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+int blocks_one(int variant) {
+    int n = 0;
+    hipError_t e;
+    if constexpr (G == 1) {
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, step_kernel<VEC, LIFE, HASH, CLIPPED>,
+                                                         kWaveLanes * kWavesPerWG, 0);
+    } else {
+        if (variant == 2)
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>,
+                                                             kWaveLanes * kWavesPerWG, 0);
+        else
+            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>,
+                                                             kWaveLanes * kWavesPerWG, 0);
+    }
+    return e == hipSuccess ? n : 0;
+}
+
+template <int VEC, int G>
+int blocks_variant(int variant, bool life, bool hash, bool clipped) {
+    if (clipped) return hash ? blocks_one<VEC, G, false, true, true>(variant) : blocks_one<VEC, G, false, false, true>(variant);
+    if (life) return hash ? blocks_one<VEC, G, true, true, false>(variant) : blocks_one<VEC, G, true, false, false>(variant);
+    return hash ? blocks_one<VEC, G, false, true, false>(variant) : blocks_one<VEC, G, false, false, false>(variant);
+}
+
+template <int G>
+int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped) {
+    switch (vec) {
+        case 4: return blocks_variant<4, G>(variant, life, hash, clipped);
+        case 2: return blocks_variant<2, G>(variant, life, hash, clipped);
+        default: return blocks_variant<1, G>(variant, life, hash, clipped);
+    }
+}
+
 template <int VEC, int G>
 hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, int gx, int gy,
                           hipStream_t st) {
@@ -727,5 +762,13 @@ hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, int, int, hi
 hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
+int blocks_step_g1(int, int, bool, bool, bool);
+int blocks_step_g2(int, int, bool, bool, bool);
+int blocks_step_g3(int, int, bool, bool, bool);
+int blocks_step_g4(int, int, bool, bool, bool);
+int blocks_step_g5(int, int, bool, bool, bool);
+int blocks_step_g6(int, int, bool, bool, bool);
+int blocks_step_g7(int, int, bool, bool, bool);
+int blocks_step_g8(int, int, bool, bool, bool);
 
 }  // namespace gol

@@ -9,4 +9,8 @@ hipError_t launch_step_g5(const StepParams& p, int vec, bool life, bool hash, bo
     return dev::launch_gens<5>(p, vec, life, hash, clipped, gx, gy, st);
 }
 
+int blocks_step_g5(int vec, int variant, bool life, bool hash, bool clipped) {
+    return dev::blocks_gens<5>(vec, variant, life, hash, clipped);
+}
+
 }  // namespace gol

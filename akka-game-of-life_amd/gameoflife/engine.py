@@ -139,6 +139,12 @@ class GolEngine:
     def profile_reset(self) -> None:
         self._chk(N.lib.gol_profile_reset(self._h))
 
+    def occupancy(self, gens_per_pass: int) -> tuple[int, int]:
+        """(resident waves per CU, strip width in words) of a G-generation pass."""
+        w, s = ctypes.c_int32(0), ctypes.c_int32(0)
+        self._chk(N.lib.gol_occupancy(self._h, gens_per_pass, ctypes.byref(w), ctypes.byref(s)))
+        return w.value, s.value
+
     def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0, words_per_lane: int = 0) -> None:
         """Performance knobs only (gol_set_tuning): rows per band, generations
         per HBM pass (1..8), words per lane (1/2/4, 0 = auto)."""

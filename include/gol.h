@@ -197,6 +197,11 @@ int gol_profile_reset(gol_ctx* ctx);
  *                   divide the words of a row). */
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane);
 
+/* Diagnostic: resident 64-lane waves per CU of the step kernel a pass of
+ * `gens_per_pass` generations would launch with the context's current
+ * tuning (occupancy API), and the strip width in words. */
+int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, int32_t* strip_words);
+
 /* Diagnostic: runs a one-wave kernel exercising the cross-lane primitives the
  * step kernel relies on (DPP wave shifts, v_alignbit, scalar loads) and
  * writes 256 words to report (layout: gol_kernels.hip selftest_kernel). */
