@@ -200,6 +200,10 @@ int stencil_variant() {
     return v;
 }
 
+// Kernel formulation a pass at `vec` words per lane actually runs: 16-byte
+// lanes always use the vertical-first kernel (gol_stencil.h kHgLanes).
+int kernel_variant(int vec) { return vec == 4 ? 1 : stencil_variant(); }
+
 // Words per lane for a single-generation pass: 16-byte lane loads where the
 // row fills whole waves of them.
 int default_vec(int64_t wwords) {
@@ -268,11 +272,12 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
 
 // Resident waves on the whole GPU for a launch (cached occupancy query).
 int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
+    const int variant = kernel_variant(vec);
     const int key = ((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
-                    stencil_variant();
+                    variant;
     auto it = ctx->occupancy_cache.find(key);
     if (it != ctx->occupancy_cache.end()) return it->second;
-    const int blocks = gol::resident_blocks_per_cu(vec, gens, stencil_variant(), life, hash, clipped);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped);
     const int64_t waves = (int64_t)blocks * gol::kWavesPerWG * ctx->num_cus;
     ctx->occupancy_cache[key] = waves;
     return waves;
@@ -324,7 +329,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
     p.birth = ctx->birth;
     p.survive = ctx->survive;
-    p.variant = stencil_variant();
+    p.variant = kernel_variant(vec);
     const int64_t waves = (int64_t)p.strips * maxbands;
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
@@ -905,7 +910,7 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
     const bool clipped = ctx->topology == GOL_REF_CLIPPED;
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int vec = lane_words(ctx, gens_per_pass);
-    const int blocks = gol::resident_blocks_per_cu(vec, gens_per_pass, stencil_variant(), life, false, clipped);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(vec), life, false, clipped);
     if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
     if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
     return GOL_OK;

@@ -675,14 +675,22 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
     }
 }
 
+// The horizontal-first kernel keeps three planes per ring row: at 16-byte
+// lanes it needs 183-270 registers or spills (1-1.6 KB scratch per lane), so
+// VEC = 4 always runs the vertical-first kernel (kernel_variant()).
+template <int VEC>
+constexpr bool kHgLanes = VEC <= 2;
+
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     if constexpr (G == 1) {
         hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
-    } else if (p.variant == 2) {
-        hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
-                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+    } else if (kHgLanes<VEC> && p.variant == 2) {
+        if constexpr (kHgLanes<VEC>) {
+            hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+                               dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+        }
     } else {
         hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
@@ -699,12 +707,15 @@ int blocks_one(int variant) {
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, step_kernel<VEC, LIFE, HASH, CLIPPED>,
                                                          kWaveLanes * kWavesPerWG, 0);
     } else {
-        if (variant == 2)
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>,
-                                                             kWaveLanes * kWavesPerWG, 0);
-        else
-            e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>,
-                                                             kWaveLanes * kWavesPerWG, 0);
+        if constexpr (kHgLanes<VEC>) {
+            if (variant == 2) {
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>,
+                                                                 kWaveLanes * kWavesPerWG, 0);
+                return e == hipSuccess ? n : 0;
+            }
+        }
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>,
+                                                         kWaveLanes * kWavesPerWG, 0);
     }
     return e == hipSuccess ? n : 0;
 }
