@@ -125,6 +125,20 @@ def roofline(kms, launches, gens_covered, cells_per_gen_per_launch):
             "generations_per_launch": gpl, "algorithmic_bytes_per_launch": algo}
 
 
+def kernel_label(info, G):
+    """Name of the kernel instance a G-generation pass launches: the strip width
+    (gol_occupancy) gives the words per lane; multi-generation passes at 8-byte
+    lanes or narrower run the horizontal-first kernel (gol_capi.cpp kernel_variant)."""
+    waves, strip = info.get(G, (0, 0))
+    if G == 1:
+        vec = strip // 64 if strip else "VEC"
+        return f"gol::dev::step_kernel<{vec},LIFE>"
+    vec = strip // 62 if strip else 0
+    name = "multistep_hg_kernel" if vec in (1, 2) and os.environ.get("GOL_STENCIL_VARIANT", "2") != "1" \
+        else "multistep_kernel"
+    return f"gol::dev::{name}<{vec or 'VEC'},{G},LIFE> ({waves} waves/CU resident)"
+
+
 def pmc_traffic(workload_key):
     """HBM bytes per launch measured with rocprofv3 --pmc (profiles/pmc_traffic.json,
     written by scripts/pmc_traffic.py with the gfx950 FETCH_SIZE x2 correction)."""
@@ -154,6 +168,7 @@ def main():
     eng.seed(0x5EED)
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    eng_info = {g: eng.occupancy(g) for g in range(1, 9)}
     value = W * H * a.steps / dt / 1e9
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
@@ -162,8 +177,7 @@ def main():
     roof = roofline(kms, launches, gcov, cells)
     key = f"{W}x{H}/N{world}/G{G}"
     if roof is not None:
-        roof["kernel"] = ("gol::dev::step_kernel<VEC,LIFE>" if G == 1
-                          else f"gol::dev::multistep_kernel<VEC,{G},LIFE>")
+        roof["kernel"] = kernel_label(eng_info, G)
         t = pmc_traffic(key)
         if t is not None:
             roof["traffic"] = t.get("hbm_bytes_per_launch")

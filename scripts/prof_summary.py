@@ -23,7 +23,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEP_KERNELS = ("step_kernel", "multistep_kernel")
+STEP_KERNELS = ("step_kernel", "multistep_kernel", "multistep_hg_kernel")
 
 
 def rows(path):
