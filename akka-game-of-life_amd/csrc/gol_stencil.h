@@ -73,6 +73,9 @@ __device__ __forceinline__ uint32_t col_mask(int64_t limit, int64_t w) {
     return (uint32_t)((1ull << (limit - lo)) - 1ull);
 }
 
+typedef uint32_t U32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
+
 template <int VEC>
 struct Words {
     uint32_t w[VEC];
@@ -94,16 +97,26 @@ __device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VE
     }
 }
 
+// Store one lane's VEC words of an output row through a buffer descriptor
+// built from the (wave-uniform) row address: lanes that do not own their
+// words and rows outside the band get an out-of-range offset / a zero-sized
+// row and the hardware bounds check drops the store.  No exec-mask branch
+// around the store, so the counted vmcnt waits of the loads that follow stay
+// exact (a skippable store makes the compiler wait for the worse path).
 template <int VEC>
-__device__ __forceinline__ void store_words(uint32_t* rp, int col, bool active, const Words<VEC>& d) {
-    if (active) {
-        if constexpr (VEC == 4) {
-            *reinterpret_cast<uint4*>(rp + col) = make_uint4(d.w[0], d.w[1], d.w[2], d.w[3]);
-        } else if constexpr (VEC == 2) {
-            *reinterpret_cast<uint2*>(rp + col) = make_uint2(d.w[0], d.w[1]);
-        } else {
-            rp[col] = d.w[0];
-        }
+__device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t row_bytes, int col, bool lane_ok,
+                                          const Words<VEC>& d) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(row, (short)0, row_ok ? row_bytes : 0, 0x00020000);
+    const int voff = lane_ok ? col * 4 : 0x7FFFFFF0;
+    if constexpr (VEC == 4) {
+        const U32x4 v = {d.w[0], d.w[1], d.w[2], d.w[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+    } else if constexpr (VEC == 2) {
+        const U32x2 v = {d.w[0], d.w[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, 0, 0);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, 0);
     }
 }
 
@@ -342,10 +355,10 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
             }
-            if (in_band) {
-                const int r = out_of(i);
-                store_words<VEC>(p.nxt + (int64_t)r * p.pitch, col, active, o);
-                if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc);
+            const int r = out_of(i);
+            store_row<VEC>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
+            if constexpr (HASH) {
+                if (in_band) hash_row<VEC>(p, r, lk1, lk2, o, acc);
             }
         };
 
@@ -472,10 +485,12 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                         // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
                         apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
                               st[s - 1][((u - s) % 3 + 3) % 3], m - 1, o);
-                    } else if (own_row) {
+                    } else {
                         const int r = brow(m);
-                        store_words<VEC>(p.nxt + (int64_t)r * p.pitch, lcol, owns, o);
-                        if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
+                        if constexpr (HASH) {
+                            if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        }
                     }
                 }
             }
@@ -656,10 +671,12 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                         if constexpr (HASH) {
                             if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
                         }
-                    } else if (own_row) {
+                    } else {
                         const int r = brow(m);
-                        store_words<VEC>(p.nxt + (int64_t)r * p.pitch, lcol, owns, o);
-                        if constexpr (HASH) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
+                        if constexpr (HASH) {
+                            if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        }
                     }
                 }
             }

@@ -10,7 +10,9 @@ import os
 import re
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgol.so")
+# GOL_LIB_PATH: an alternative build of the same library, for A/B timing
+# experiments only (scripts/ab_build.sh); products use the in-tree build.
+LIB_PATH = os.environ.get("GOL_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libgol.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "gol.h")
 
 GOL_OK = 0
