@@ -52,6 +52,7 @@ struct gol_ctx {
     int32_t topology = GOL_TORUS;
     uint32_t birth = 0, survive = 0;
     int64_t vis_w = 0, vis_h = 0;
+    bool pairs = false;  // device words pair-interleaved (torus, even words per row)
     int device = 0;
     int vec_fixed = 0;  // words per lane forced by gol_set_tuning (0: per-pass automatic)
     // device state
@@ -214,9 +215,10 @@ int default_vec(int64_t wwords) {
 // carry 62 output lanes, so a row of w words needs ceil(w / (62 v)) strips;
 // prefer 16-byte lanes unless 8-byte lanes waste clearly fewer lanes.
 int lane_words(const gol_ctx* ctx, int gens) {
-    if (ctx->vec_fixed > 0) return ctx->vec_fixed;
+    // the pair layout needs whole pairs per lane: 8- or 16-byte lanes
+    if (ctx->vec_fixed > 0) return ctx->pairs ? std::max(ctx->vec_fixed, 2) : ctx->vec_fixed;
     const int64_t w = ctx->wwords;
-    if (gens == 1) return default_vec(w);
+    if (gens == 1) return ctx->pairs ? std::max(default_vec(w), 2) : default_vec(w);
     auto util = [&](int v) -> double {
         const int64_t strips = (w / v + 61) / 62;
         return (double)(w / v) / (double)(strips * 64);
@@ -224,9 +226,9 @@ int lane_words(const gol_ctx* ctx, int gens) {
     const bool ok4 = w % 4 == 0 && w >= 4 * 62, ok2 = w % 2 == 0 && w >= 2 * 62;
     // the horizontal-first kernel keeps 3 planes per ring row: 8-byte lanes
     // (95 VGPRs at G = 6, 5 waves/SIMD) beat 16-byte lanes (183 VGPRs, 2 waves)
-    if (stencil_variant() == 2) return ok2 ? 2 : 1;
+    if (stencil_variant() == 2) return ok2 || ctx->pairs ? 2 : 1;
     if (ok4 && (!ok2 || util(4) >= util(2) - 0.03)) return 4;
-    if (ok2) return 2;
+    if (ok2 || ctx->pairs) return 2;
     return 1;
 }
 
@@ -273,11 +275,11 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
 // Resident waves on the whole GPU for a launch (cached occupancy query).
 int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
     const int variant = kernel_variant(vec);
-    const int key = ((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
-                    variant;
+    const int key = (((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
+                     variant) * 2 + (ctx->pairs ? 1 : 0);
     auto it = ctx->occupancy_cache.find(key);
     if (it != ctx->occupancy_cache.end()) return it->second;
-    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped, ctx->pairs);
     const int64_t waves = (int64_t)blocks * gol::kWavesPerWG * ctx->num_cus;
     ctx->occupancy_cache[key] = waves;
     return waves;
@@ -338,7 +340,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, gx, n, ctx->compute));
+    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, n, ctx->compute));
     if (ev) {
         HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
         ctx->prof_gens += (uint64_t)gens;
@@ -622,6 +624,7 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     ctx->survive = c.survive_mask;
     ctx->vis_w = c.vis_width > 0 ? c.vis_width : c.width - 1;
     ctx->vis_h = c.vis_height > 0 ? c.vis_height : c.height - 1;
+    ctx->pairs = c.topology == GOL_TORUS && wwords % 2 == 0;
     ctx->device = c.device;
     ctx->vec_fixed = 0;
     if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess)
@@ -678,7 +681,7 @@ int gol_seed(gol_ctx* ctx, uint64_t seed) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (int rc = bind(ctx)) return rc;
     HIP_CHECK(ctx, gol::launch_seed(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->width, ctx->row0,
-                                    (int32_t)ctx->rows, seed, ctx->compute));
+                                    (int32_t)ctx->rows, seed, ctx->pairs, ctx->compute));
     ctx->epoch = 0;
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     return GOL_OK;
@@ -697,8 +700,13 @@ int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words) {
                 return set_err(ctx, GOL_EINVAL, "padding bits beyond width set in row %lld", (long long)r);
     }
     if (int rc = bind(ctx)) return rc;
-    HIP_CHECK(ctx, hipMemcpy2DAsync(ctx->plane[ctx->cur], ctx->pitch * 4, packed, host_pitch_words * 4,
-                                    (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyHostToDevice, ctx->compute));
+    // pair layout: upload into the spare plane, interleave into the current one
+    uint32_t* dst = ctx->pairs ? ctx->plane[ctx->cur ^ 1] : ctx->plane[ctx->cur];
+    HIP_CHECK(ctx, hipMemcpy2DAsync(dst, ctx->pitch * 4, packed, host_pitch_words * 4, (size_t)ctx->wwords * 4,
+                                    ctx->rows, hipMemcpyHostToDevice, ctx->compute));
+    if (ctx->pairs)
+        HIP_CHECK(ctx, gol::launch_convert(dst, ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, (int32_t)ctx->rows,
+                                           true, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     ctx->epoch = 0;
     return GOL_OK;
@@ -768,8 +776,16 @@ int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words) {
     if (!ctx || !packed_out) return set_err(ctx, GOL_EINVAL, "null argument");
     if (host_pitch_words < ctx->wwords) return set_err(ctx, GOL_EINVAL, "host pitch too small");
     if (int rc = bind(ctx)) return rc;
-    HIP_CHECK(ctx, hipMemcpy2DAsync(packed_out, host_pitch_words * 4, ctx->plane[ctx->cur], ctx->pitch * 4,
-                                    (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyDeviceToHost, ctx->compute));
+    // pair layout: de-interleave into the spare plane (free between passes:
+    // the compute stream is ordered after every reader of the last pass)
+    const uint32_t* src = ctx->plane[ctx->cur];
+    if (ctx->pairs) {
+        HIP_CHECK(ctx, gol::launch_convert(src, ctx->plane[ctx->cur ^ 1], ctx->pitch, ctx->wwords,
+                                           (int32_t)ctx->rows, false, ctx->compute));
+        src = ctx->plane[ctx->cur ^ 1];
+    }
+    HIP_CHECK(ctx, hipMemcpy2DAsync(packed_out, host_pitch_words * 4, src, ctx->pitch * 4, (size_t)ctx->wwords * 4,
+                                    ctx->rows, hipMemcpyDeviceToHost, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     return GOL_OK;
 }
@@ -779,11 +795,15 @@ int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state) {
     if (x < 0 || x >= ctx->width || y < ctx->row0 || y >= ctx->row0 + ctx->rows)
         return set_err(ctx, GOL_EINVAL, "cell (%lld, %lld) not in this shard", (long long)x, (long long)y);
     if (int rc = bind(ctx)) return rc;
+    // row-major: bit x % 32 of word x / 32; pairs: bit (x % 64) / 2 of word
+    // 2 (x / 64) + x % 2
+    const int64_t word = ctx->pairs ? 2 * (x / 64) + (x & 1) : x / 32;
+    const int bit = ctx->pairs ? (int)((x % 64) >> 1) : (int)(x % 32);
     uint32_t w = 0;
-    HIP_CHECK(ctx, hipMemcpyAsync(&w, ctx->plane[ctx->cur] + (y - ctx->row0) * ctx->pitch + x / 32, 4,
+    HIP_CHECK(ctx, hipMemcpyAsync(&w, ctx->plane[ctx->cur] + (y - ctx->row0) * ctx->pitch + word, 4,
                                   hipMemcpyDeviceToHost, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-    *state = (int)((w >> (x % 32)) & 1u);
+    *state = (int)((w >> bit) & 1u);
     return GOL_OK;
 }
 
@@ -910,7 +930,8 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
     const bool clipped = ctx->topology == GOL_REF_CLIPPED;
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int vec = lane_words(ctx, gens_per_pass);
-    const int blocks = gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(vec), life, false, clipped);
+    const int blocks =
+        gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(vec), life, false, clipped, ctx->pairs);
     if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
     if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
     return GOL_OK;

@@ -51,17 +51,23 @@ int strip_words(int vec, int gens);
 
 // vec: words per lane (1, 2 or 4); gens: generations per pass; life: B3/S23
 // fast path (torus only); hash: fuse the per-generation state hash; clipped:
-// reference geometry.
-hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped,
+// reference geometry; pairs: the plane is pair-interleaved (even vec only).
+hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, bool pairs,
                        int grid_x, int grid_y, hipStream_t stream);
 
 // Resident 256-thread workgroups per CU of the step kernel instance a launch
 // with these parameters uses (hipOccupancyMaxActiveBlocksPerMultiprocessor);
 // 0 if unknown.
-int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped);
+int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, bool pairs);
 
+// Seeded board in the device layout (pairs: pair-interleaved words).
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width,
-                       int64_t grow0, int32_t rows, uint64_t seed, hipStream_t stream);
+                       int64_t grow0, int32_t rows, uint64_t seed, bool pairs, hipStream_t stream);
+
+// Row-major words <-> pair-interleaved words, `rows` rows of `wwords` (even)
+// words, `pitch` words apart in both planes (src != dst).
+hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
+                          bool to_pairs, hipStream_t stream);
 
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0,
                        int32_t rows, unsigned long long* slots, hipStream_t stream);

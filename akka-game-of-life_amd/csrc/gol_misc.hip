@@ -16,17 +16,69 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
+// Pair layout (DESIGN.md "Data layout"; oracle/gol_oracle.c oracle_to_pairs):
+// row-major words (w0, w1) = columns 0..31, 32..63 of a pair <-> (e, o) =
+// its even and odd columns.
+__device__ __forceinline__ uint32_t even_bits(uint32_t x) {  // bits 0, 2, .., 30 -> 0 .. 15
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+__device__ __forceinline__ uint32_t spread_bits(uint32_t x) {  // bits 0 .. 15 -> 0, 2, .., 30
+    x &= 0x0000FFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
 // oracle/gol_oracle.c oracle_seed_packed, on device: the seeded stand-in for
-// BoardCreator.scala:23 (Random.nextBoolean() per cell).
+// BoardCreator.scala:23 (Random.nextBoolean() per cell).  With `pairs` each
+// thread derives its device word from the two row-major words of its pair.
 __global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0,
-                            int32_t rows, uint64_t seed) {
+                            int32_t rows, uint64_t seed, int pairs) {
     const int64_t total = (int64_t)rows * wwords;
+    auto word = [&](int64_t r, int64_t c) -> uint32_t {
+        const uint64_t i = (uint64_t)(grow0 + r) * (uint64_t)wwords + (uint64_t)c;
+        const uint64_t z = splitmix64(seed + 0x9E3779B97F4A7C15ull * (i + 1));
+        return (uint32_t)(z >> 32) & dev::col_mask(width, c);
+    };
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = k / wwords, c = k % wwords;
-        const uint64_t i = (uint64_t)(grow0 + r) * (uint64_t)wwords + (uint64_t)c;
-        const uint64_t z = splitmix64(seed + 0x9E3779B97F4A7C15ull * (i + 1));
-        plane[r * pitch + c] = (uint32_t)(z >> 32) & dev::col_mask(width, c);
+        uint32_t w;
+        if (pairs) {
+            const int64_t c0 = c & ~(int64_t)1;
+            const uint32_t w0 = word(r, c0), w1 = word(r, c0 + 1);
+            const int sh = (int)(c & 1);  // even columns: bits 0, 2, ..; odd: 1, 3, ..
+            w = even_bits(w0 >> sh) | (even_bits(w1 >> sh) << 16);
+        } else {
+            w = word(r, c);
+        }
+        plane[r * pitch + c] = w;
+    }
+}
+
+__global__ void convert_kernel(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t npairs, int32_t rows,
+                               int to_pairs) {
+    const int64_t total = (int64_t)rows * npairs;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = k / npairs, c = 2 * (k % npairs);
+        const uint2 in = *reinterpret_cast<const uint2*>(src + r * pitch + c);
+        uint2 out;
+        if (to_pairs) {
+            out.x = even_bits(in.x) | (even_bits(in.y) << 16);
+            out.y = even_bits(in.x >> 1) | (even_bits(in.y >> 1) << 16);
+        } else {
+            out.x = spread_bits(in.x) | (spread_bits(in.y) << 1);
+            out.y = spread_bits(in.x >> 16) | (spread_bits(in.y >> 16) << 1);
+        }
+        *reinterpret_cast<uint2*>(dst + r * pitch + c) = out;
     }
 }
 
@@ -64,41 +116,51 @@ __global__ void selftest_kernel(const uint32_t* in, uint32_t* out) {
 
 int strip_words(int vec, int gens) { return (gens == 1 ? kWaveLanes : kWaveLanes - 2) * vec; }
 
-hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, int grid_x,
-                       int grid_y, hipStream_t stream) {
+hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, bool pairs,
+                       int grid_x, int grid_y, hipStream_t stream) {
     switch (gens) {
-        case 1: return launch_step_g1(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 2: return launch_step_g2(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 3: return launch_step_g3(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 4: return launch_step_g4(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 5: return launch_step_g5(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 6: return launch_step_g6(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 7: return launch_step_g7(p, vec, life, hash, clipped, grid_x, grid_y, stream);
-        case 8: return launch_step_g8(p, vec, life, hash, clipped, grid_x, grid_y, stream);
+        case 1: return launch_step_g1(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 2: return launch_step_g2(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 3: return launch_step_g3(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 4: return launch_step_g4(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 5: return launch_step_g5(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 6: return launch_step_g6(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 7: return launch_step_g7(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 8: return launch_step_g8(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
-int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped) {
+int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, bool pairs) {
     switch (gens) {
-        case 1: return blocks_step_g1(vec, variant, life, hash, clipped);
-        case 2: return blocks_step_g2(vec, variant, life, hash, clipped);
-        case 3: return blocks_step_g3(vec, variant, life, hash, clipped);
-        case 4: return blocks_step_g4(vec, variant, life, hash, clipped);
-        case 5: return blocks_step_g5(vec, variant, life, hash, clipped);
-        case 6: return blocks_step_g6(vec, variant, life, hash, clipped);
-        case 7: return blocks_step_g7(vec, variant, life, hash, clipped);
-        case 8: return blocks_step_g8(vec, variant, life, hash, clipped);
+        case 1: return blocks_step_g1(vec, variant, life, hash, clipped, pairs);
+        case 2: return blocks_step_g2(vec, variant, life, hash, clipped, pairs);
+        case 3: return blocks_step_g3(vec, variant, life, hash, clipped, pairs);
+        case 4: return blocks_step_g4(vec, variant, life, hash, clipped, pairs);
+        case 5: return blocks_step_g5(vec, variant, life, hash, clipped, pairs);
+        case 6: return blocks_step_g6(vec, variant, life, hash, clipped, pairs);
+        case 7: return blocks_step_g7(vec, variant, life, hash, clipped, pairs);
+        case 8: return blocks_step_g8(vec, variant, life, hash, clipped, pairs);
         default: return 0;
     }
 }
 
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0, int32_t rows,
-                       uint64_t seed, hipStream_t stream) {
+                       uint64_t seed, bool pairs, hipStream_t stream) {
     const int64_t total = (int64_t)rows * wwords;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
     hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(256), 0, stream, plane, pitch, wwords, width, grow0, rows,
-                       seed);
+                       seed, pairs ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
+                          bool to_pairs, hipStream_t stream) {
+    if (wwords % 2 != 0) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)rows * (wwords / 2);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
+    hipLaunchKernelGGL(convert_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, pitch, wwords / 2, rows,
+                       to_pairs ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -35,6 +35,8 @@
 //                    live only in registers (one 3-row ring per stage) and
 //                    are hashed there; G-row halos come from above/below.
 #pragma once
+#include <type_traits>
+
 #include "gol_kernels.h"
 
 namespace gol {
@@ -182,21 +184,42 @@ __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC
 // B3/S23: next = (n == 3) | (alive & n == 2) = ~qq & (pp ^ c0) & (n0 | alive)
 // (pp ^ c0 = 1 means exactly one of pp, c0 is set, so bit 2 is qq; n = 8 has
 // pp = c0 = 0 and dies) -- two v_bitop3 after the adder.
-template <int VEC, bool LIFE>
+//
+// PAIRS (pair-interleaved words, DESIGN.md "Data layout"): word j even holds
+// the even columns of a 64-column pair, word j+1 the odd ones, so column x-1
+// of an even-column word is the odd word shifted up one bit (the bit shifted
+// in is the previous pair's last odd column) and column x+1 is the odd word
+// itself; mirror-wise for odd-column words.  One funnel shift per word
+// instead of two (v_alignbit issues at half the rate of v_bitop3 on gfx950).
+template <int VEC, bool LIFE, bool PAIRS>
 __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (&v0)[VEC],
                                            const uint32_t (&v1)[VEC], const uint32_t (&p0)[VEC],
                                            const uint32_t (&p1)[VEC], uint32_t m0, uint32_t m1, uint32_t n0,
                                            uint32_t n1, const Words<VEC>& alive, Words<VEC>& out) {
+    static_assert(!PAIRS || VEC % 2 == 0, "the pair layout needs whole pairs per lane");
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
         const uint32_t l0 = j == 0 ? m0 : v0[j - 1];
         const uint32_t l1 = j == 0 ? m1 : v1[j - 1];
         const uint32_t r0 = j == VEC - 1 ? n0 : v0[j + 1];
         const uint32_t r1 = j == VEC - 1 ? n1 : v1[j + 1];
-        const uint32_t w0 = __builtin_amdgcn_alignbit(v0[j], l0, 31);  // column x-1
-        const uint32_t e0 = __builtin_amdgcn_alignbit(r0, v0[j], 1);   // column x+1
-        const uint32_t w1 = __builtin_amdgcn_alignbit(v1[j], l1, 31);
-        const uint32_t e1 = __builtin_amdgcn_alignbit(r1, v1[j], 1);
+        uint32_t w0, e0, w1, e1;
+        if (!PAIRS) {
+            w0 = __builtin_amdgcn_alignbit(v0[j], l0, 31);  // column x-1
+            e0 = __builtin_amdgcn_alignbit(r0, v0[j], 1);   // column x+1
+            w1 = __builtin_amdgcn_alignbit(v1[j], l1, 31);
+            e1 = __builtin_amdgcn_alignbit(r1, v1[j], 1);
+        } else if (j % 2 == 0) {  // even columns: r = the pair's odd word, l = previous odd word
+            w0 = __builtin_amdgcn_alignbit(r0, l0, 31);
+            w1 = __builtin_amdgcn_alignbit(r1, l1, 31);
+            e0 = r0;
+            e1 = r1;
+        } else {  // odd columns: l = the pair's even word, r = next even word
+            w0 = l0;
+            w1 = l1;
+            e0 = __builtin_amdgcn_alignbit(r0, l0, 1);
+            e1 = __builtin_amdgcn_alignbit(r1, l1, 1);
+        }
         const uint32_t nb0 = GOL_BITOP3(w0, e0, p0[j], kXor3);
         const uint32_t c0 = GOL_BITOP3(w0, e0, p0[j], kMaj);
         const uint32_t pp = GOL_BITOP3(w1, e1, p1[j], kXor3);
@@ -260,7 +283,7 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
 // --------------------------------------------------------------------------
 // One generation per pass.
 // --------------------------------------------------------------------------
-template <int VEC, bool LIFE, bool HASH, bool CLIPPED>
+template <int VEC, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
@@ -350,7 +373,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 n1 = last ? r1 : n1;
             }
             Words<VEC> o;
-            rule_words<VEC, LIFE>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
+            rule_words<VEC, LIFE, PAIRS>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -385,7 +408,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
 // --------------------------------------------------------------------------
 // G generations per pass (temporal blocking).
 // --------------------------------------------------------------------------
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(const StepParams p) {
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
@@ -456,7 +479,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             const uint32_t m1 = dpp_shr1_zero(v1[VEC - 1]);
             const uint32_t n0 = dpp_shl1_zero(v0[0]);
             const uint32_t n1 = dpp_shl1_zero(v1[0]);
-            rule_words<VEC, LIFE>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
+            rule_words<VEC, LIFE, PAIRS>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -526,7 +549,7 @@ struct HRow {
     uint32_t a[CLIPPED ? VEC : 1];       // clipped: the real row (alive bits)
 };
 
-template <int VEC, bool CLIPPED>
+template <int VEC, bool CLIPPED, bool PAIRS>
 __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const uint32_t (&cmask)[VEC],
                                        HRow<VEC, CLIPPED>& o) {
     uint32_t rv[VEC];
@@ -537,6 +560,22 @@ __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const ui
     }
     const uint32_t left = dpp_shr1_zero(rv[VEC - 1]);  // halo lanes read zeros at the wave's ends
     const uint32_t right = dpp_shl1_zero(rv[0]);
+    if constexpr (PAIRS) {  // (e, o) pairs: see rule_words
+        static_assert(VEC % 2 == 0 && !CLIPPED, "pair layout");
+#pragma unroll
+        for (int j = 0; j < VEC; j += 2) {
+            const uint32_t e = rv[j], od = rv[j + 1];
+            const uint32_t we = __builtin_amdgcn_alignbit(od, j == 0 ? left : rv[j - 1], 31);
+            const uint32_t eo = __builtin_amdgcn_alignbit(j + 2 == VEC ? right : rv[j + 2], e, 1);
+            o.h0[j] = GOL_BITOP3(we, e, od, kXor3);
+            o.h1[j] = GOL_BITOP3(we, e, od, kMaj);
+            o.h0[j + 1] = GOL_BITOP3(e, od, eo, kXor3);
+            o.h1[j + 1] = GOL_BITOP3(e, od, eo, kMaj);
+            o.r[j] = e;
+            o.r[j + 1] = od;
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
         const uint32_t w = __builtin_amdgcn_alignbit(rv[j], j == 0 ? left : rv[j - 1], 31);
@@ -584,7 +623,7 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
     }
 }
 
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(const StepParams p) {
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
@@ -656,7 +695,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                 const int q = q0 + u;
                 load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
                 // input row q arrives at ring 0
-                arrive<VEC, CLIPPED>(in[u], vis(q), cmask, hr[0][u % 3]);
+                arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
                 for (int s = 1; s <= G; ++s) {
                     // stage s: stream row m = q - s from ring s-1 rows m-1, m, m+1
@@ -667,7 +706,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                                                 hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
                     const bool own_row = m >= G && m < n_in - G;
                     if (s < G) {
-                        arrive<VEC, CLIPPED>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
+                        arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
                         if constexpr (HASH) {
                             if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
                         }
@@ -698,83 +737,99 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 template <int VEC>
 constexpr bool kHgLanes = VEC <= 2;
 
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     if constexpr (G == 1) {
-        hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+        hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
     } else if (kHgLanes<VEC> && p.variant == 2) {
         if constexpr (kHgLanes<VEC>) {
-            hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+            hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
                                dim3(kWaveLanes * kWavesPerWG), 0, st, p);
         }
     } else {
-        hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>), dim3(gx, gy),
+        hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
     }
     return hipGetLastError();
 }
 
 // Resident 256-thread workgroups per CU for a kernel instance (occupancy API).
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 int blocks_one(int variant) {
     int n = 0;
     hipError_t e;
     if constexpr (G == 1) {
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, step_kernel<VEC, LIFE, HASH, CLIPPED>,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>,
                                                          kWaveLanes * kWavesPerWG, 0);
     } else {
         if constexpr (kHgLanes<VEC>) {
             if (variant == 2) {
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED>,
-                                                                 kWaveLanes * kWavesPerWG, 0);
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, kWaveLanes * kWavesPerWG, 0);
                 return e == hipSuccess ? n : 0;
             }
         }
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED>,
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>,
                                                          kWaveLanes * kWavesPerWG, 0);
     }
     return e == hipSuccess ? n : 0;
 }
 
+// The instances a launch can select: clipped boards (generic rule, row-major
+// words), tori (B3/S23 fast path or generic rule) in row-major or pair layout
+// (even lane widths only).  `F` is called with the instance's template
+// arguments as std::integral_constant values.
+template <int VEC, typename F>
+auto dispatch_kind(bool life, bool hash, bool clipped, bool pairs, F&& f) {
+    using T = std::true_type;
+    using N = std::false_type;
+    if (clipped) return hash ? f(N{}, T{}, T{}, N{}) : f(N{}, N{}, T{}, N{});
+    if (pairs) {
+        if constexpr (VEC % 2 == 0) {
+            if (life) return hash ? f(T{}, T{}, N{}, T{}) : f(T{}, N{}, N{}, T{});
+            return hash ? f(N{}, T{}, N{}, T{}) : f(N{}, N{}, N{}, T{});
+        }
+    }
+    if (life) return hash ? f(T{}, T{}, N{}, N{}) : f(T{}, N{}, N{}, N{});
+    return hash ? f(N{}, T{}, N{}, N{}) : f(N{}, N{}, N{}, N{});
+}
+
 template <int VEC, int G>
-int blocks_variant(int variant, bool life, bool hash, bool clipped) {
-    if (clipped) return hash ? blocks_one<VEC, G, false, true, true>(variant) : blocks_one<VEC, G, false, false, true>(variant);
-    if (life) return hash ? blocks_one<VEC, G, true, true, false>(variant) : blocks_one<VEC, G, true, false, false>(variant);
-    return hash ? blocks_one<VEC, G, false, true, false>(variant) : blocks_one<VEC, G, false, false, false>(variant);
+int blocks_variant(int variant, bool life, bool hash, bool clipped, bool pairs) {
+    if (pairs && VEC % 2 != 0) return 0;
+    return dispatch_kind<VEC>(life, hash, clipped, pairs, [&](auto L, auto H, auto C, auto P) {
+        return blocks_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(P)::value>(
+            variant);
+    });
 }
 
 template <int G>
-int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped) {
+int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped, bool pairs) {
     switch (vec) {
-        case 4: return blocks_variant<4, G>(variant, life, hash, clipped);
-        case 2: return blocks_variant<2, G>(variant, life, hash, clipped);
-        default: return blocks_variant<1, G>(variant, life, hash, clipped);
+        case 4: return blocks_variant<4, G>(variant, life, hash, clipped, pairs);
+        case 2: return blocks_variant<2, G>(variant, life, hash, clipped, pairs);
+        default: return blocks_variant<1, G>(variant, life, hash, clipped, pairs);
     }
 }
 
 template <int VEC, int G>
-hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, int gx, int gy,
+hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, bool pairs, int gx, int gy,
                           hipStream_t st) {
-    if (clipped) {
-        return hash ? launch_one<VEC, G, false, true, true>(p, gx, gy, st)
-                    : launch_one<VEC, G, false, false, true>(p, gx, gy, st);
-    }
-    if (life) {
-        return hash ? launch_one<VEC, G, true, true, false>(p, gx, gy, st)
-                    : launch_one<VEC, G, true, false, false>(p, gx, gy, st);
-    }
-    return hash ? launch_one<VEC, G, false, true, false>(p, gx, gy, st)
-                : launch_one<VEC, G, false, false, false>(p, gx, gy, st);
+    if (pairs && VEC % 2 != 0) return hipErrorInvalidValue;  // checked by the host layer
+    return dispatch_kind<VEC>(life, hash, clipped, pairs, [&](auto L, auto H, auto C, auto P) {
+        return launch_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(P)::value>(
+            p, gx, gy, st);
+    });
 }
 
 template <int G>
-hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool clipped, int gx, int gy,
+hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool clipped, bool pairs, int gx, int gy,
                        hipStream_t st) {
     switch (vec) {
-        case 4: return launch_variant<4, G>(p, life, hash, clipped, gx, gy, st);
-        case 2: return launch_variant<2, G>(p, life, hash, clipped, gx, gy, st);
-        case 1: return launch_variant<1, G>(p, life, hash, clipped, gx, gy, st);
+        case 4: return launch_variant<4, G>(p, life, hash, clipped, pairs, gx, gy, st);
+        case 2: return launch_variant<2, G>(p, life, hash, clipped, pairs, gx, gy, st);
+        case 1: return launch_variant<1, G>(p, life, hash, clipped, pairs, gx, gy, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -782,21 +837,21 @@ hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool 
 }  // namespace dev
 
 // Defined one per translation unit (gol_step_g<G>.hip).
-hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, int, int, hipStream_t);
-int blocks_step_g1(int, int, bool, bool, bool);
-int blocks_step_g2(int, int, bool, bool, bool);
-int blocks_step_g3(int, int, bool, bool, bool);
-int blocks_step_g4(int, int, bool, bool, bool);
-int blocks_step_g5(int, int, bool, bool, bool);
-int blocks_step_g6(int, int, bool, bool, bool);
-int blocks_step_g7(int, int, bool, bool, bool);
-int blocks_step_g8(int, int, bool, bool, bool);
+hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+int blocks_step_g1(int, int, bool, bool, bool, bool);
+int blocks_step_g2(int, int, bool, bool, bool, bool);
+int blocks_step_g3(int, int, bool, bool, bool, bool);
+int blocks_step_g4(int, int, bool, bool, bool, bool);
+int blocks_step_g5(int, int, bool, bool, bool, bool);
+int blocks_step_g6(int, int, bool, bool, bool, bool);
+int blocks_step_g7(int, int, bool, bool, bool, bool);
+int blocks_step_g8(int, int, bool, bool, bool, bool);
 
 }  // namespace gol

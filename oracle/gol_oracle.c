@@ -280,23 +280,56 @@ void oracle_step_packed(const uint32_t* cur, uint32_t* nxt, int64_t W, int64_t H
 /* State hash (sharding-invariant, order-independent).                  */
 /* ------------------------------------------------------------------ */
 
-/* For every word i = y * wwords + c of the global board (wwords = ceil(W/32)):
+/* Device word order (DESIGN.md "Data layout"): a torus whose rows hold an
+ * even number of words is stored pair-interleaved -- columns 64k .. 64k+63 of
+ * a row live in words 2k (the even columns: bit b = column 64k + 2b) and
+ * 2k+1 (the odd columns: bit b = column 64k + 2b + 1).  Every other board is
+ * stored row-major (bit x % 32 of word x / 32).  The hash is defined over
+ * the device words, so the engine hashes without converting. */
+int oracle_pair_layout(int topology, int64_t wwords) {
+    return topology == ORACLE_TORUS && wwords % 2 == 0;
+}
+
+static uint32_t even_bits(uint32_t x) { /* bits 0, 2, .., 30 -> bits 0 .. 15 */
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+
+/* Row-major pair (w0 = columns 0..31, w1 = 32..63) -> (even, odd) words. */
+void oracle_to_pairs(uint32_t w0, uint32_t w1, uint32_t* e, uint32_t* o) {
+    *e = even_bits(w0) | (even_bits(w1) << 16);
+    *o = even_bits(w0 >> 1) | (even_bits(w1 >> 1) << 16);
+}
+
+/* For every device word i = y * wwords + c of the global board (wwords = ceil(W/32)):
  *   g  = (uint32)(i mod 2^32)
  *   k1 = g * 0x9E3779B9,  k2 = (g * 0x85EBCA6B) | 1          (mod 2^32)
  *   term = (uint64)(word ^ k1) * (uint64)k2
  * hash = sum of terms mod 2^64.  A sum commutes, so the value is the same for
  * one shard or many and for any evaluation order; any single-word difference
  * always changes it (x -> (x ^ k1) * k2 is injective for odd k2).
- * Here: rows [row0, row0+rows) of a board with `wwords` words per row. */
+ * Here: rows [row0, row0+rows) of a row-major board with `wwords` words per
+ * row; `pairs` hashes its pair-interleaved device words instead. */
 uint64_t oracle_hash_packed(const uint32_t* board, int64_t wwords, int64_t row0, int64_t rows,
-                            int64_t pitch) {
+                            int64_t pitch, int pairs) {
     uint64_t h = 0;
     for (int64_t r = 0; r < rows; ++r) {
         for (int64_t c = 0; c < wwords; ++c) {
+            uint32_t word = board[r * pitch + c];
+            if (pairs) {
+                const int64_t c0 = c & ~(int64_t)1;
+                uint32_t e, o;
+                oracle_to_pairs(board[r * pitch + c0], board[r * pitch + c0 + 1], &e, &o);
+                word = (c & 1) ? o : e;
+            }
             uint32_t g = (uint32_t)((uint64_t)(row0 + r) * (uint64_t)wwords + (uint64_t)c);
             uint32_t k1 = g * 0x9E3779B9u;
             uint32_t k2 = (g * 0x85EBCA6Bu) | 1u;
-            h += (uint64_t)(board[r * pitch + c] ^ k1) * (uint64_t)k2;
+            h += (uint64_t)(word ^ k1) * (uint64_t)k2;
         }
     }
     return h;
@@ -309,11 +342,12 @@ void oracle_run_packed(uint32_t* board, uint32_t* tmp, int64_t W, int64_t H, int
                        int topology, uint32_t birth, uint32_t survive, int64_t vis_w,
                        int64_t vis_h, int64_t gens, uint64_t* hashes, int nthreads) {
     const int64_t wwords = (W + 31) / 32;
+    const int pairs = oracle_pair_layout(topology, wwords);
     uint32_t* a = board;
     uint32_t* b = tmp;
     for (int64_t g = 0; g < gens; ++g) {
         oracle_step_packed(a, b, W, H, pitch, topology, birth, survive, vis_w, vis_h, nthreads);
-        if (hashes) hashes[g] = oracle_hash_packed(b, wwords, 0, H, pitch);
+        if (hashes) hashes[g] = oracle_hash_packed(b, wwords, 0, H, pitch, pairs);
         uint32_t* t = a; a = b; b = t;
     }
     if (a != board) memcpy(board, a, (size_t)(H * pitch) * sizeof(uint32_t));

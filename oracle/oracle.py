@@ -68,7 +68,8 @@ def lib():
         L.oracle_step_packed.argtypes = [_u32p, _u32p, _i64, _i64, _i64, ctypes.c_int,
                                          ctypes.c_uint32, ctypes.c_uint32, _i64, _i64, ctypes.c_int]
         L.oracle_hash_packed.restype = ctypes.c_uint64
-        L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64]
+        L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64, ctypes.c_int]
+        L.oracle_pair_layout.argtypes = [ctypes.c_int, _i64]
         L.oracle_run_packed.argtypes = [_u32p, _u32p, _i64, _i64, _i64, ctypes.c_int,
                                         ctypes.c_uint32, ctypes.c_uint32, _i64, _i64, _i64,
                                         _u64p, ctypes.c_int]
@@ -160,18 +161,47 @@ def run_packed(packed: np.ndarray, W: int, gens: int, topology: int = TORUS, rul
     return board, hashes
 
 
-def hash_packed(packed: np.ndarray, W: int, row0: int = 0) -> int:
+def pair_layout(W: int, topology: int = TORUS) -> bool:
+    """True when the engine stores the board pair-interleaved (gol_oracle.c
+    oracle_pair_layout): a torus with an even number of words per row."""
+    return bool(lib().oracle_pair_layout(topology, wwords(W)))
+
+
+def hash_packed(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
+    """State hash of row-major packed rows [row0, row0 + rows) of a board
+    (over its device words: pair-interleaved for even-width tori)."""
     packed = np.ascontiguousarray(packed, dtype=np.uint32)
     rows, pitch = packed.shape
-    return int(lib().oracle_hash_packed(_p(packed, _u32p), wwords(W), row0, rows, pitch))
+    return int(lib().oracle_hash_packed(_p(packed, _u32p), wwords(W), row0, rows, pitch,
+                                        int(pair_layout(W, topology))))
 
 
 # ------------------------------------------------- independent numpy restatement
 
-def np_hash(packed: np.ndarray, W: int, row0: int = 0) -> int:
+def np_device_words(packed: np.ndarray, W: int, topology: int = TORUS) -> np.ndarray:
+    """Row-major packed rows -> the engine's device words (independent numpy
+    restatement of the layout rule: an even-width torus is pair-interleaved,
+    column 64k + 2b -> bit b of word 2k, column 64k + 2b + 1 -> bit b of
+    word 2k + 1)."""
+    ww = wwords(W)
+    p = np.asarray(packed, dtype=np.uint32)[:, :ww]
+    if not (topology == TORUS and ww % 2 == 0):
+        return p.copy()
+    rows = p.shape[0]
+    bits = ((p[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(rows, ww // 2, 64)
+    weights = np.uint64(1) << np.arange(32, dtype=np.uint64)
+    even = (bits[:, :, 0::2].astype(np.uint64) * weights).sum(axis=2)
+    odd = (bits[:, :, 1::2].astype(np.uint64) * weights).sum(axis=2)
+    out = np.empty((rows, ww), dtype=np.uint32)
+    out[:, 0::2] = even.astype(np.uint32)
+    out[:, 1::2] = odd.astype(np.uint32)
+    return out
+
+
+def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
     """Same hash spec as gol_oracle.c, written independently with numpy."""
     ww = wwords(W)
-    p = np.asarray(packed, dtype=np.uint64)[:, :ww]
+    p = np_device_words(packed, W, topology).astype(np.uint64)
     rows = p.shape[0]
     g = ((np.arange(rows, dtype=np.uint64)[:, None] + np.uint64(row0)) * np.uint64(ww)
          + np.arange(ww, dtype=np.uint64)[None, :]) & np.uint64(0xFFFFFFFF)

@@ -13,6 +13,6 @@ else
   git -C "$ROOT" archive "$rev" akka-game-of-life_amd/csrc akka-game-of-life_amd/Makefile include | tar -x -C "$D/tmp"
 fi
 mv "$D/tmp/akka-game-of-life_amd"/* "$D/pkg/"; mv "$D/tmp/include"/* "$D/include/"; rm -rf "$D/tmp"
-make -C "$D/pkg" -j8 lib/libgol.so >/dev/null
+make -C "$D/pkg" -j8 lib/libgol.so EXTRA_HIPFLAGS="$EXTRA_HIPFLAGS" >/dev/null
 mkdir -p "$D/lib"; mv "$D/pkg/lib/libgol.so" "$D/lib/"; rm -rf "$D/pkg/build"
 echo "$D/lib/libgol.so"

@@ -1,0 +1,99 @@
+// VALU issue-rate microbenchmark for the instruction mix of the step kernel:
+// independent chains of v_bitop3 / v_alignbit / DPP wave shifts, several
+// waves per SIMD, timed with hipEvents.  Prints wave-instructions per cycle
+// per SIMD at the clock measured with s_memtime / s_memrealtime.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+constexpr int kIters = 4096;
+
+template <int MODE, int CH>
+__global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned long long* clk) {
+    uint32_t a[CH], b[CH], c[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) { a[i] = seed * (threadIdx.x + i); b[i] = a[i] ^ 0x9e3779b9u; c[i] = a[i] + 17u; }
+    unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < kIters; ++it) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            if constexpr (MODE == 0) {  // 4 bitop3
+                a[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0x96);
+                b[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0xe8);
+                c[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0x06);
+                a[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0xe0);
+            } else if constexpr (MODE == 1) {  // 4 alignbit
+                a[i] = __builtin_amdgcn_alignbit(a[i], b[i], 31);
+                b[i] = __builtin_amdgcn_alignbit(c[i], a[i], 1);
+                c[i] = __builtin_amdgcn_alignbit(b[i], a[i], 31);
+                a[i] = __builtin_amdgcn_alignbit(c[i], b[i], 1);
+            } else if constexpr (MODE == 2) {  // 2 DPP wave shifts + 2 bitop3
+                a[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)a[i], 0x138, 0xf, 0xf, true) ^ b[i];
+                b[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0x96);
+                c[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)b[i], 0x130, 0xf, 0xf, true) ^ a[i];
+                a[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0xe8);
+            } else {  // step-kernel mix: 1 DPP, 2 alignbit, 9 bitop3, 1 xor  (13)
+                const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[i], 0x138, 0xf, 0xf, true);
+                const uint32_t w = __builtin_amdgcn_alignbit(a[i], l, 31);
+                const uint32_t e = __builtin_amdgcn_alignbit(b[i], a[i], 1);
+                const uint32_t h0 = __builtin_amdgcn_bitop3_b32(w, a[i], e, 0x96);
+                const uint32_t h1 = __builtin_amdgcn_bitop3_b32(w, a[i], e, 0xe8);
+                const uint32_t g0 = h0 ^ c[i];
+                const uint32_t g1 = __builtin_amdgcn_bitop3_b32(h1, h0, c[i], 0xd0);
+                const uint32_t n0 = __builtin_amdgcn_bitop3_b32(b[i], h0, g0, 0x96);
+                const uint32_t c0 = __builtin_amdgcn_bitop3_b32(b[i], h0, g0, 0xe8);
+                const uint32_t pp = __builtin_amdgcn_bitop3_b32(c[i], h1, g1, 0x96);
+                const uint32_t qq = __builtin_amdgcn_bitop3_b32(c[i], h1, g1, 0xe8);
+                const uint32_t x = __builtin_amdgcn_bitop3_b32(qq, pp, c0, 0x06);
+                c[i] = b[i]; b[i] = a[i];
+                a[i] = __builtin_amdgcn_bitop3_b32(x, n0, a[i], 0xe0);
+            }
+        }
+    }
+    unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) acc ^= a[i] ^ b[i] ^ c[i];
+    out[blockIdx.x * 256 + threadIdx.x] = acc;
+    if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
+}
+
+template <int MODE, int CH>
+int run(const char* name, int ops_per_chain_iter, int waves_per_simd, uint32_t* out, unsigned long long* clk, int cus) {
+    const int blocks = cus * waves_per_simd;  // 256-thread WG = 4 waves = 1 per SIMD
+    hipEvent_t e0, e1;
+    CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((k<MODE, CH>), dim3(blocks), dim3(256), 0, 0, out, 1u, clk);
+    CHK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+        CHK(hipEventRecord(e0));
+        hipLaunchKernelGGL((k<MODE, CH>), dim3(blocks), dim3(256), 0, 0, out, 1u + r, clk);
+        CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+        float ms; CHK(hipEventElapsedTime(&ms, e0, e1)); if (ms < best) best = ms;
+    }
+    unsigned long long h[2]; CHK(hipMemcpy(h, clk, sizeof h, hipMemcpyDeviceToHost));
+    const double ghz = (double)h[0] / (double)h[1] * 0.1;  // memrealtime = 100 MHz
+    const double wave_instr = (double)blocks * 4 * kIters * CH * ops_per_chain_iter;
+    const double per_simd_per_cycle = wave_instr / (cus * 4.0) / (best * 1e-3 * ghz * 1e9);
+    printf("%-28s waves/SIMD=%d chains=%2d  %.3f ms  clk=%.2f GHz  wave-VALU/cycle/SIMD=%.3f  lane-ops/s=%.1fT\n", name,
+           waves_per_simd, CH, best, ghz, per_simd_per_cycle, wave_instr * 64 / (best * 1e-3) / 1e12);
+    return 0;
+}
+
+int main() {
+    int cus = 0; hipDeviceProp_t prop; CHK(hipGetDeviceProperties(&prop, 0)); cus = prop.multiProcessorCount;
+    uint32_t* out; unsigned long long* clk;
+    CHK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4)); CHK(hipMalloc(&clk, 16));
+    for (int w : {1, 2, 4, 5, 8}) {
+        run<0, 4>("bitop3 x4", 4, w, out, clk, cus);
+        run<1, 4>("alignbit x4", 4, w, out, clk, cus);
+        run<2, 4>("dpp+xor/bitop3", 4, w, out, clk, cus);
+        run<3, 2>("step mix (13 ops)", 13, w, out, clk, cus);
+        run<3, 4>("step mix (13 ops)", 13, w, out, clk, cus);
+    }
+    return 0;
+}

@@ -97,10 +97,27 @@ def test_blinker_block_glider_torus():
     assert (O.unpack(p, W) == glider).all()  # full wrap after 4N generations
 
 
+def test_pair_layout_rule():
+    # device words are pair-interleaved exactly for tori of even word width
+    assert O.pair_layout(64) and O.pair_layout(320) and not O.pair_layout(32) and not O.pair_layout(96)
+    assert not O.pair_layout(64, O.REF_CLIPPED)
+    # numpy restatement of the interleave: column 64k + 2b -> bit b of word 2k, 64k + 2b + 1 -> word 2k + 1
+    cells = np.random.default_rng(3).integers(0, 2, size=(5, 192), dtype=np.uint8)
+    dev = O.np_device_words(O.pack(cells), 192)
+    for y in range(5):
+        for x in range(192):
+            word, bit = 2 * (x // 64) + (x & 1), (x % 64) >> 1
+            assert (int(dev[y, word]) >> bit) & 1 == cells[y, x]
+
+
 def test_hash_properties():
+    for W, topo in [(320, O.TORUS), (352, O.TORUS), (320, O.REF_CLIPPED), (300, O.REF_CLIPPED)]:
+        b = O.seed_packed(W, 40, 1)
+        assert O.hash_packed(b, W, topology=topo) == O.np_hash(b, W, topology=topo)
     b = O.seed_packed(320, 40, 1)
     h = O.hash_packed(b, 320)
     assert h == O.np_hash(b, 320)
+    assert h != O.hash_packed(b, 320, topology=O.REF_CLIPPED)  # pair-interleaved vs row-major words
     # sharding invariance: partial hashes of row blocks sum to the whole
     parts = [O.hash_packed(b[r0:r1], 320, row0=r0) for r0, r1 in [(0, 7), (7, 30), (30, 40)]]
     assert sum(parts) % (1 << 64) == h

@@ -64,7 +64,7 @@ def _worker(rank, world, port, torus, out_q):
                 # ext row k is global row row0-1+k; visible iff global < H-1
                 nxt = O.step_packed(ext, W, O.REF_CLIPPED, O.LIFE, vis=(W - 1, H - row0))[1:-1]
             shard = nxt
-            part = O.hash_packed(shard, W, row0=row0)
+            part = O.hash_packed(shard, W, row0=row0, topology=O.TORUS if torus else O.REF_CLIPPED)
             t = torch.tensor([part - (1 << 64) if part >= (1 << 63) else part], dtype=torch.int64)
             dist.all_reduce(t)  # int64 sum wraps like uint64
             hashes.append(int(t.item()) & ((1 << 64) - 1))
