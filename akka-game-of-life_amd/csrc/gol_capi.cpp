@@ -66,7 +66,8 @@ struct gol_ctx {
     std::vector<unsigned long long> host_slots;
     uint64_t epoch = 0;
     hipStream_t compute = nullptr, comm = nullptr;
-    hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+    hipStream_t edge = nullptr;  // boundary-row kernels of a sharded pass (concurrent with the interior)
+    hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
     // RCCL
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
@@ -291,7 +292,8 @@ int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bo
 // is the dominant kernel.
 int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
                   const uint32_t* hbot, int64_t halo_stride, bool wrap_y, unsigned long long* slots, int n,
-                  const int32_t* lo, const int32_t* hi, bool main_launch) {
+                  const int32_t* lo, const int32_t* hi, bool main_launch, hipStream_t stream = nullptr) {
+    if (!stream) stream = ctx->compute;
     gol::StepParams p{};
     p.cur = cur;
     p.nxt = nxt;
@@ -340,7 +342,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, n, ctx->compute));
+    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, n, stream));
     if (ev) {
         HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
         ctx->prof_gens += (uint64_t)gens;
@@ -348,11 +350,15 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     return GOL_OK;
 }
 
-// Kernels of one sharded pass: the interior rows [G, rows-G) first -- they
-// need no halo and overlap the exchange -- then, once every event in
-// `halo_ready` has fired, the two boundary row blocks.  A missing neighbour
-// (clipped board ends) reads dead rows: zero_row holds kMaxGensPerPass of
-// them at the halo pitch.
+// Kernels of one sharded pass: the interior rows [G, rows-G) -- they need no
+// halo and overlap the exchange -- on the compute stream, and the two
+// boundary row blocks on the edge stream once every event in `halo_ready`
+// has fired.  The boundary launch runs concurrently with the tail of the
+// interior one (its waves take the slots the interior's waves free) instead
+// of after it; the compute stream then waits for it, so the next pass, a
+// snapshot or a hash sees the whole plane.  A missing neighbour (clipped
+// board ends) reads dead rows: zero_row holds kMaxGensPerPass of them at the
+// halo pitch.
 int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
                          const hipEvent_t* halo_ready, int nready) {
     uint32_t* cur = ctx->plane[ctx->cur];
@@ -365,9 +371,16 @@ int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool ha
         const int32_t lo[1] = {G}, hi[1] = {rows - G};
         int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
         if (rc) return rc;
-        for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
+        // The exchange events follow this pass's ev_ready, recorded on the
+        // compute stream after the previous pass's boundary rows: every
+        // reader of the plane the boundary kernels overwrite has finished.
+        for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->edge, halo_ready[k], 0));
         const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
-        return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false);
+        rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false, ctx->edge);
+        if (rc) return rc;
+        HIP_CHECK(ctx, hipEventRecord(ctx->ev_edge, ctx->edge));
+        HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_edge, 0));
+        return GOL_OK;
     }
     for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
     const int32_t lo[1] = {0}, hi[1] = {rows};
@@ -515,6 +528,7 @@ void destroy_impl(gol_ctx* c) {
     hipSetDevice(c->device);
     if (c->compute) hipStreamSynchronize(c->compute);
     if (c->comm) hipStreamSynchronize(c->comm);
+    if (c->edge) hipStreamSynchronize(c->edge);
     if (c->nccl) ncclCommDestroy(c->nccl);
     for (auto& e : c->evs) {
         if (e.start) hipEventDestroy(e.start);
@@ -522,6 +536,7 @@ void destroy_impl(gol_ctx* c) {
     }
     if (c->ev_ready) hipEventDestroy(c->ev_ready);
     if (c->ev_halo) hipEventDestroy(c->ev_halo);
+    if (c->ev_edge) hipEventDestroy(c->ev_edge);
     for (auto* p : c->plane) if (p) hipFree(p);
     if (c->halo_top) hipFree(c->halo_top);
     if (c->halo_bot) hipFree(c->halo_bot);
@@ -529,6 +544,7 @@ void destroy_impl(gol_ctx* c) {
     if (c->slots) hipFree(c->slots);
     if (c->compute) hipStreamDestroy(c->compute);
     if (c->comm) hipStreamDestroy(c->comm);
+    if (c->edge) hipStreamDestroy(c->edge);
     delete c;
 }
 
@@ -662,6 +678,8 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     }
     if (hipStreamCreateWithFlags(&ctx->compute, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->comm, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->edge, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_edge, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_ready, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_halo, hipEventDisableTiming) != hipSuccess) {
         set_err(ctx, GOL_EHIP, "stream/event creation failed");
