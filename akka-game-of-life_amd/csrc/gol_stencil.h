@@ -44,7 +44,7 @@ namespace dev {
 
 constexpr int kPF = 2;               // step_kernel: rows prefetched ahead
 constexpr int kRing = kPF + 3;       // step_kernel: register ring of stream rows
-constexpr int kMPF = 3;              // multistep_kernel: rows prefetched ahead
+constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
 constexpr int kMRing = 6;            // multistep_kernel: input ring (multiple of 3)
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
