@@ -135,6 +135,13 @@ def device_count() -> int:
     return n.value
 
 
+def pair_layout(width: int, topology: int = GOL_TORUS) -> bool:
+    """True when libgol keeps the board pair-interleaved in HBM (gol_capi.cpp
+    gol_create: a torus with an even number of 32-bit words per row); the
+    state hash is defined over those device words."""
+    return topology == GOL_TORUS and ((width + 31) // 32) % 2 == 0
+
+
 def shard_rows(height: int, rank: int, nranks: int) -> tuple[int, int]:
     r0, rows = ctypes.c_int64(0), ctypes.c_int64(0)
     check(lib.gol_shard_rows(height, rank, nranks, ctypes.byref(r0), ctypes.byref(rows)))

@@ -139,6 +139,28 @@ def kernel_label(info, G):
     return f"gol::dev::{name}<{vec or 'VEC'},{G},LIFE> ({waves} waves/CU resident)"
 
 
+# Issue-cost model of the multi-generation kernel (DESIGN.md "Roofline"):
+# VALU instructions per 32-cell word and generation in the loop of
+# multistep_hg_kernel<2, G, LIFE> on the pair layout (from its ISA), and the
+# measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
+VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_xor_b32": (1, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
+SIMDS = 256 * 4
+CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md max clock
+
+
+def valu_roofline(gcups):
+    """Cell-update rate the VALU issue model allows at the max clock (every
+    SIMD issuing the loop's instruction mix back to back), and the fraction
+    of it the run reached.  Halo lanes and band halo rows are overheads
+    counted against the kernel, not removed from the peak."""
+    cycles = sum(n * c for n, c in VALU_MIX.values())
+    peak = SIMDS * CLOCK_GHZ * 1e9 / cycles * 64 * 32 / 1e9
+    return {"bound": "valu", "instructions_per_word_generation": {k: n for k, (n, _) in VALU_MIX.items()},
+            "cycles_per_word_generation": round(cycles, 2), "clock_ghz": CLOCK_GHZ,
+            "peak_gcups": round(peak, 1), "frac": round(gcups / peak, 4),
+            "source": "profiles/r01_valu_op_costs.txt (scripts/micro/op_cost.hip)"}
+
+
 def pmc_traffic(workload_key):
     """HBM bytes per launch measured with rocprofv3 --pmc (profiles/pmc_traffic.json,
     written by scripts/pmc_traffic.py with the gfx950 FETCH_SIZE x2 correction)."""
@@ -178,6 +200,9 @@ def main():
     key = f"{W}x{H}/N{world}/G{G}"
     if roof is not None:
         roof["kernel"] = kernel_label(eng_info, G)
+        if "multistep_hg_kernel<2," in roof["kernel"] and N.pair_layout(W):
+            # per-launch rate of the dominant kernel, not the wall-clock value
+            roof["valu"] = valu_roofline(cells * gcov / launches / (roof["avg_launch_ms"] * 1e-3) / 1e9)
         t = pmc_traffic(key)
         if t is not None:
             roof["traffic"] = t.get("hbm_bytes_per_launch")

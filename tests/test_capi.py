@@ -104,3 +104,12 @@ def test_codec_matches_oracle_layout():
         assert p.dtype == np.uint32 and p.shape == (H, (W + 31) // 32)
         assert (p == O.pack(c)).all()
         assert (codec.unpack(p, W) == c).all()
+
+
+def test_pair_layout_rule_matches_oracle():
+    # the host mirror of gol_create's layout rule and the oracle's hash layout agree
+    from gameoflife import _native as N
+    from oracle import oracle as O
+    for w in (32, 64, 96, 128, 320, 352, 992, 1024, 4096, 65536, 262144):
+        assert N.pair_layout(w) == O.pair_layout(w, O.TORUS)
+        assert not N.pair_layout(w, N.GOL_REF_CLIPPED) and not O.pair_layout(w, O.REF_CLIPPED)
