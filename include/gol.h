@@ -19,10 +19,15 @@
  *   - There is no CPU fallback: a context can only be created on a HIP
  *     device; without one gol_create() fails with GOL_ENODEV.
  *
- * Board layout in HBM: bit-packed rows, row = y, bit (x % 32) of 32-bit word
- * (x / 32) is cell x (LSB first); words per row = ceil(width / 32); bits at
- * x >= width are zero.  Two device planes (current / next) are swapped after
- * every generation.
+ * Host buffers (gol_load, gol_snapshot, checkpoints): bit-packed rows,
+ * row = y, bit (x % 32) of 32-bit word (x / 32) is cell x (LSB first); words
+ * per row = ceil(width / 32); bits at x >= width are zero.
+ * Device layout (internal): the same rows, except that a torus with an even
+ * number of words per row is kept pair-interleaved -- word 2k holds the even
+ * columns of columns 64k..64k+63 (bit b = column 64k + 2b), word 2k+1 the odd
+ * ones.  The state hash is defined over these device words (DESIGN.md
+ * "State hash").  Two device planes (current / next) are swapped after every
+ * pass.
  */
 #ifndef GOL_H
 #define GOL_H

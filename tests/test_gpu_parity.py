@@ -227,20 +227,40 @@ def test_snapshot_get_cell_checkpoint(gpu):
         np.testing.assert_array_equal(e.step(5, hashes=True), ref)
 
 
+@pytest.mark.parametrize("W", [32 * 70, 32 * 71])  # pair-interleaved / row-major device words
+def test_get_cell_every_layout(gpu, W):
+    H = 37
+    rng = np.random.default_rng(W)
+    with engine(W, H) as e:
+        e.seed(11)
+        e.step(13)  # default pass depth (6) plus a remainder pass
+        cells = O.unpack(e.snapshot(), W)
+        for _ in range(200):
+            x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
+            assert e.get_cell(x, y) == bool(cells[y, x]), (x, y)
+        for x in (0, 1, 31, 32, 63, 64, 65, W - 2, W - 1):
+            assert e.get_cell(x, 5) == bool(cells[5, x]), x
+
+
 def test_full_size_65536_bit_exact(gpu):
-    """BASELINE.json config 3 geometry (65536^2 torus): 3 generations checked
-    word-for-word against the multithreaded CPU oracle."""
+    """BASELINE.json config 3 geometry (65536^2 torus): 6 generations checked
+    word-for-word against the multithreaded CPU oracle, including one pass of
+    the automatic depth (6) the benchmark runs."""
     W = H = 65536
     board = O.seed_packed(W, H, 0x5EED)
-    final_cpu, want = O.run_packed(board, W, 4, O.TORUS, O.LIFE)
-    for gpp in (1, 2, 4):
+    final_cpu, want = O.run_packed(board, W, 6, O.TORUS, O.LIFE)
+    for gpp in (1, 2, 4, 0):
         with engine(W, H) as e:
             e.set_tuning(gens_per_pass=gpp)
             e.seed(0x5EED)
-            got = e.step(4, hashes=True)
+            got = e.step(6, hashes=True)
             final = e.snapshot()
         np.testing.assert_array_equal(got, want)
         assert (final == final_cpu).all(), gpp
+    with engine(W, H) as e:  # the benchmark's own path: no fused hash
+        e.seed(0x5EED)
+        e.step(6)
+        assert (e.snapshot() == final_cpu).all()
 
 
 def test_known_patterns_on_gpu(gpu):
