@@ -273,6 +273,46 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
     return (int)band;
 }
 
+// Tail split of a pass's rows (DESIGN.md §4 "Band schedule").  The
+// dispatcher hands workgroups to CUs as slots free up, so a pass of a few
+// rounds of resident waves ends with uneven per-SIMD tails: the CUs that got
+// the last full-height bands finish late.  The last `frac` x resident waves
+// therefore cover their rows in bands of band / div, dispatched after the
+// bulk.  Default: one resident round's worth of waves in bands of band / 3
+// (profiles/r01_tail_sweep.txt, reseeded boards, min of 4 rounds: +4 % on the
+// N = 8 per-rank shape 262144 x 32768, +2 % at x 65536, +1 % at x 131072 and
+// 262144^2, neutral at 65536^2).  GOL_TAIL="frac,div" overrides it (A/B
+// sweeps, scripts/tail_sweep.py); frac 0 disables it.
+struct TailSplit {
+    int32_t rows = 0;  // rows at the end of the range in short bands (0: none)
+    int32_t band = 0;
+};
+
+constexpr double kTailFrac = 1.0;
+constexpr int kTailDiv = 3;
+
+TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int64_t resident) {
+    double frac = kTailFrac;
+    int div = kTailDiv;
+    const char* env = getenv("GOL_TAIL");
+    if (env && *env) {
+        if (sscanf(env, "%lf,%d", &frac, &div) != 2) frac = 0.0;
+    } else if (ctx->band_rows > 0) {
+        return {};  // a fixed band (tuning) is taken literally
+    }
+    TailSplit t;
+    if (frac <= 0.0 || div < 2 || resident <= 0 || strips <= 0) return t;
+    const int64_t waves = (rows + band - 1) / band * strips;
+    if (waves <= resident) return t;  // a single round: nothing to even out
+    const int b2 = std::max(8, band / div);
+    int64_t trows = (int64_t)(frac * (double)resident / strips) * b2;
+    trows = std::min<int64_t>(trows, rows / 2) / b2 * b2;
+    if (trows <= 0) return t;
+    t.rows = (int32_t)trows;
+    t.band = b2;
+    return t;
+}
+
 // Resident waves on the whole GPU for a launch (cached occupancy query).
 int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
     const int variant = kernel_variant(vec);
@@ -317,24 +357,36 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     const bool clipped = ctx->topology == GOL_REF_CLIPPED;
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int64_t resident = (n == 1 && gens > 1) ? resident_waves(ctx, vec, gens, life, slots != nullptr, clipped) : 0;
-    p.band = pick_band(ctx, maxlen, p.strips, gens, resident);
-    int maxbands = 0;
-    for (int k = 0; k < 2; ++k) {
-        if (k < n) {
-            p.row_lo[k] = lo[k];
-            p.row_hi[k] = hi[k];
-            p.nbands[k] = (hi[k] - lo[k] + p.band - 1) / p.band;
-        } else {
-            p.row_lo[k] = p.row_hi[k] = p.nbands[k] = 0;
-        }
-        maxbands = std::max(maxbands, p.nbands[k]);
+    const int band = pick_band(ctx, maxlen, p.strips, gens, resident);
+    int32_t rlo[2] = {0, 0}, rhi[2] = {0, 0}, rband[2] = {band, band};
+    int nr = n;
+    for (int k = 0; k < n; ++k) {
+        rlo[k] = lo[k];
+        rhi[k] = hi[k];
     }
-    if (maxbands == 0) return GOL_OK;
+    if (n == 1 && gens > 1) {
+        const TailSplit t = tail_split(ctx, hi[0] - lo[0], p.strips, band, resident);
+        if (t.rows > 0) {  // bulk [lo, hi - t.rows) in `band` rows, tail in t.band rows
+            nr = 2;
+            rhi[0] = hi[0] - t.rows;
+            rlo[1] = rhi[0];
+            rhi[1] = hi[0];
+            rband[1] = t.band;
+        }
+    }
+    int64_t waves = 0;
+    for (int k = 0; k < 2; ++k) {
+        p.row_lo[k] = rlo[k];
+        p.row_hi[k] = rhi[k];
+        p.band[k] = rband[k];
+        p.nbands[k] = k < nr ? (rhi[k] - rlo[k] + rband[k] - 1) / rband[k] : 0;
+        waves += (int64_t)p.nbands[k] * p.strips;
+    }
+    if (waves == 0) return GOL_OK;
     p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
     p.birth = ctx->birth;
     p.survive = ctx->survive;
     p.variant = kernel_variant(vec);
-    const int64_t waves = (int64_t)p.strips * maxbands;
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
     if (ctx->prof && main_launch) {
@@ -342,7 +394,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, n, stream));
+    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, 1, stream));
     if (ev) {
         HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
         ctx->prof_gens += (uint64_t)gens;

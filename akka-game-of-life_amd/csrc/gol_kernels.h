@@ -18,8 +18,10 @@ constexpr uint32_t kHashK1 = 0x9E3779B9u;
 constexpr uint32_t kHashK2 = 0x85EBCA6Bu;
 
 // One launch advances G generations (G = `gens`, 1..kMaxGensPerPass) over up
-// to two local row ranges (blockIdx.y selects one): the whole shard, or the
-// interior / the two boundary row blocks of a sharded pass.
+// to two local row ranges, each cut into bands of its own height: the whole
+// shard (one range, or a bulk range plus a tail of shorter bands), or the two
+// boundary row blocks of a sharded pass.  Waves are numbered range 0's bands
+// first, then range 1's (the order the dispatcher hands them out).
 struct StepParams {
     const uint32_t* cur;       // local row 0 of the current plane
     uint32_t* nxt;             // local row 0 of the next plane
@@ -36,7 +38,7 @@ struct StepParams {
     int32_t row_lo[2];
     int32_t row_hi[2];
     int32_t nbands[2];
-    int32_t band;              // output rows streamed by one wave
+    int32_t band[2];           // output rows streamed by one wave, per range
     int32_t strips;            // column strips per row
     int32_t wrap_x;            // torus in x
     int32_t wrap_y;            // unsharded torus: local rows wrap modulo `rows`

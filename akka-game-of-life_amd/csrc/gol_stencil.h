@@ -36,6 +36,7 @@
 //                    are hashed there; G-row halos come from above/below.
 #pragma once
 #include <type_traits>
+#include <utility>
 
 #include "gol_kernels.h"
 
@@ -48,6 +49,19 @@ constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
 constexpr int kMRing = 6;            // multistep_kernel: input ring (multiple of 3)
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N-1>): a loop
+// whose index is a compile-time constant in every copy, whatever the
+// unroller's size heuristics (register-ring slots must never be indexed at
+// run time, or the rings move to scratch).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
     return (m & a) | (~m & b);
@@ -120,6 +134,18 @@ __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t ro
     } else {
         __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, 0);
     }
+}
+
+// Wave -> (row range, column strip, band of the range): range 0's bands
+// come first, then range 1's (StepParams).  Wave-uniform.
+struct WaveTile {
+    int range, strip, band;
+};
+__device__ __forceinline__ WaveTile wave_tile(const StepParams& p, int wave) {
+    const int n0 = p.nbands[0] * p.strips;
+    const int range = wave >= n0 ? 1 : 0;
+    const int w = range ? wave - n0 : wave;
+    return {range, w % p.strips, w / p.strips};
 }
 
 // Local row pointer for r in [-G, rows + G).
@@ -276,7 +302,7 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
         unsigned long long t = 0;
 #pragma unroll
         for (int w = 0; w < kWavesPerWG; ++w) t += part[w];
-        atomicAdd(slots + (size_t)((blockIdx.x + blockIdx.y) % kHashSlots) * kHashSlotStride, t);
+        atomicAdd(slots + (size_t)(blockIdx.x % kHashSlots) * kHashSlotStride, t);
     }
 }
 
@@ -287,15 +313,13 @@ template <int VEC, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
-    const int rg = blockIdx.y;
-    const int strip = wave % p.strips;
-    const int bandi = wave / p.strips;
+    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc = 0;
 
     if (bandi < p.nbands[rg]) {
-        const int r_begin = p.row_lo[rg] + bandi * p.band;
-        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
+        const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
         const int nrows = r_end - r_begin;
         const int s0 = strip * (kWaveLanes * VEC);
         const int nact = min(kWaveLanes, (p.wwords - s0) / VEC);
@@ -415,17 +439,15 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
     constexpr int kOut = (kWaveLanes - 2) * VEC;  // output words per strip
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
-    const int rg = blockIdx.y;
-    const int strip = wave % p.strips;
-    const int bandi = wave / p.strips;
+    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
     for (int s = 0; s < G; ++s) acc[s] = 0;
 
     if (bandi < p.nbands[rg]) {
-        const int r_begin = p.row_lo[rg] + bandi * p.band;
-        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
+        const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
         const int nrows = r_end - r_begin;
         const int n_in = nrows + 2 * G;  // stream rows r_begin-G .. r_end+G-1
         const int s0 = strip * kOut;
@@ -486,37 +508,40 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             }
         };
 
+        // Stream row q (slot u = q % kMRing): prefetch row q + kMPF, stage s
+        // produces stream row q - s.
+        auto row_step = [&](const int q, const int u) {
+            load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
+            // stage 1: stream row q-1 from input rows q-2, q-1, q
+            Words<VEC> o;
+            apply(in[(u + kMRing - 2) % kMRing], in[(u + kMRing - 1) % kMRing], in[u], q - 1, o);
+#pragma unroll
+            for (int s = 1; s <= G; ++s) {
+                const int m = q - s;  // stream row produced by stage s
+                const bool own_row = m >= G && m < n_in - G;
+                if (s < G) {
+                    st[s - 1][((u - s) % 3 + 3) % 3] = o;
+                    if constexpr (HASH) {
+                        if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                    }
+                    // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
+                    apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
+                          st[s - 1][((u - s) % 3 + 3) % 3], m - 1, o);
+                } else {
+                    const int r = brow(m);
+                    store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
+                    if constexpr (HASH) {
+                        if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                    }
+                }
+            }
+        };
+
 #pragma unroll
         for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
         for (int q0 = 0; q0 < n_in; q0 += kMRing) {
 #pragma unroll
-            for (int u = 0; u < kMRing; ++u) {
-                const int q = q0 + u;
-                load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
-                // stage 1: stream row q-1 from input rows q-2, q-1, q
-                Words<VEC> o;
-                apply(in[(u + kMRing - 2) % kMRing], in[(u + kMRing - 1) % kMRing], in[u], q - 1, o);
-#pragma unroll
-                for (int s = 1; s <= G; ++s) {
-                    const int m = q - s;  // stream row produced by stage s
-                    const bool own_row = m >= G && m < n_in - G;
-                    if (s < G) {
-                        st[s - 1][((u - s) % 3 + 3) % 3] = o;
-                        if constexpr (HASH) {
-                            if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
-                        }
-                        // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
-                        apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
-                              st[s - 1][((u - s) % 3 + 3) % 3], m - 1, o);
-                    } else {
-                        const int r = brow(m);
-                        store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
-                        if constexpr (HASH) {
-                            if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
-                        }
-                    }
-                }
-            }
+            for (int u = 0; u < kMRing; ++u) row_step(q0 + u, u);
         }
         if (!owns) {
 #pragma unroll
@@ -630,17 +655,15 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
     constexpr int kOut = (kWaveLanes - 2) * VEC;
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const int wave = blockIdx.x * kWavesPerWG + wave_in_wg;
-    const int rg = blockIdx.y;
-    const int strip = wave % p.strips;
-    const int bandi = wave / p.strips;
+    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
     for (int s = 0; s < G; ++s) acc[s] = 0;
 
     if (bandi < p.nbands[rg]) {
-        const int r_begin = p.row_lo[rg] + bandi * p.band;
-        const int r_end = min(r_begin + p.band, p.row_hi[rg]);
+        const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
+        const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
         const int nrows = r_end - r_begin;
         const int n_in = nrows + 2 * G;
         const int s0 = strip * kOut;
@@ -687,38 +710,55 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 
         auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
 
+        // Stream row q (ring slot u = q % kMRing): prefetch row q + kMPF,
+        // input row q arrives at ring 0, stage s produces stream row q - s.
+        // Stage s has valid inputs only from q = 2s on (its rows m < s are
+        // built from the clamped rows before the band and are never stored,
+        // hashed or read by a valid row), so the pipeline fill -- the first
+        // kFill rows, q known at compile time -- skips those stage steps.
+        auto row_step = [&](const int q, const int u, const bool fill) {
+            load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
+            arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
-        for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
-        for (int q0 = 0; q0 < n_in; q0 += kMRing) {
-#pragma unroll
-            for (int u = 0; u < kMRing; ++u) {
-                const int q = q0 + u;
-                load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
-                // input row q arrives at ring 0
-                arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
-#pragma unroll
-                for (int s = 1; s <= G; ++s) {
-                    // stage s: stream row m = q - s from ring s-1 rows m-1, m, m+1
-                    const int m = q - s;
-                    Words<VEC> o;
-                    rule_hg<VEC, LIFE, CLIPPED>(p, hr[s - 1][((u - s - 1) % 3 + 3) % 3],
-                                                hr[s - 1][((u - s) % 3 + 3) % 3],
-                                                hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
-                    const bool own_row = m >= G && m < n_in - G;
-                    if (s < G) {
-                        arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
-                        if constexpr (HASH) {
-                            if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
-                        }
-                    } else {
-                        const int r = brow(m);
-                        store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
-                        if constexpr (HASH) {
-                            if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
-                        }
+            for (int s = 1; s <= G; ++s) {
+                if (fill && q < 2 * s) break;  // stages s.. have no valid row yet
+                // stage s: stream row m = q - s from ring s-1 rows m-1, m, m+1
+                const int m = q - s;
+                Words<VEC> o;
+                rule_hg<VEC, LIFE, CLIPPED>(p, hr[s - 1][((u - s - 1) % 3 + 3) % 3],
+                                            hr[s - 1][((u - s) % 3 + 3) % 3],
+                                            hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
+                const bool own_row = m >= G && m < n_in - G;
+                if (s < G) {
+                    arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
+                    if constexpr (HASH) {
+                        if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                    }
+                } else {
+                    const int r = brow(m);
+                    store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
+                    if constexpr (HASH) {
+                        if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
                     }
                 }
             }
+        };
+
+#pragma unroll
+        for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
+        constexpr int kFill = (2 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
+        // The peeled fill is one long straight-line block; only the B3/S23
+        // instances keep their rings in registers through it (the generic-rule
+        // mux tree, and the per-generation hash sums at G > 6, make the
+        // scheduler spill), so they alone skip the dead fill steps.
+        int q_begin = 0;
+        if constexpr (LIFE && (!HASH || G <= 6)) {
+            static_for<kFill>([&](auto Q) { row_step(Q.value, Q.value % kMRing, true); });
+            q_begin = kFill;
+        }
+        for (int q0 = q_begin; q0 < n_in; q0 += kMRing) {
+#pragma unroll
+            for (int u = 0; u < kMRing; ++u) row_step(q0 + u, u, false);
         }
         if (!owns) {
 #pragma unroll

@@ -172,6 +172,27 @@ def pmc_traffic(workload_key):
         return None
 
 
+def secondary_run(GolEngine, torch, dist, a, local):
+    """BASELINE.json configs[2]: the 65536^2 single-GPU roofline run."""
+    S = 65536
+    with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
+        e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
+        e2.seed(0x5EED)
+        # SURVEY.md section 8(d) config 3: >= 10 warm-up and >= 100 timed
+        # generations, rounded up to whole 6-generation passes
+        n2, w2 = max(a.steps, 102), max(a.warmup, 12)
+        dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
+    r2 = roofline(kms2, l2, g2, S * S)
+    if r2 is not None:
+        t = pmc_traffic(f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
+        if t is not None:
+            r2["traffic"] = t.get("hbm_bytes_per_launch")
+            r2["traffic_source"] = t.get("source")
+    return {"workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
+            "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": w2,
+            "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2}
+
+
 def main():
     a = parse()
     torch, dist, rank, world, local = dist_setup(a.gpus)
@@ -179,6 +200,11 @@ def main():
     from gameoflife.engine import GolEngine
 
     W = H = a.board
+    # configs[2] (65536^2, N = 1 only) first: a board allocated after the
+    # 16 GiB one was freed stepped ~5 % slower (scripts/alloc_order.py).
+    secondary = None
+    if rank == 0 and world == 1 and not a.no_secondary:
+        secondary = secondary_run(GolEngine, torch, dist, a, local)
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
     eng.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
@@ -231,23 +257,8 @@ def main():
     eng.close()
 
     if rank == 0 and world == 1:
-        if not a.no_secondary:
-            S = 65536
-            with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
-                e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
-                e2.seed(0x5EED)
-                n2 = max(a.steps, 24)
-                dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, a.warmup, a.hash)
-                r2 = roofline(kms2, l2, g2, S * S)
-                if r2 is not None:
-                    t = pmc_traffic(f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
-                    if t is not None:
-                        r2["traffic"] = t.get("hbm_bytes_per_launch")
-                        r2["traffic_source"] = t.get("source")
-                out["secondary"] = {
-                    "workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
-                    "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS",
-                    "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2}
+        if secondary is not None:
+            out["secondary"] = secondary
         if not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
     if rank == 0:

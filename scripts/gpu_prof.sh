@@ -1,6 +1,7 @@
 # Profiling round: rocprofv3 kernel-trace/stats of the bench command itself,
 # an unprofiled bench run, and separate PMC passes (FETCH_SIZE, WRITE_SIZE)
-# for HBM traffic at G = 6 (auto) and G = 1.
+# for HBM traffic at G = 6 (auto) and G = 1, and one pass of clock / VALU-issue
+# counters (scripts/pmc_clock.py).
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 P=gpurun_out/prof
@@ -19,5 +20,11 @@ for edge in 262144 65536; do
       [ $rc -eq 0 ] || exit $rc
     done
   done
+done
+for edge in 262144 65536; do
+  timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+    -T -d $P/pmc_clock_$edge -o run --output-format csv -- python3 scripts/prof_run.py $edge 60 0 > $P/pmc_clock_$edge.log 2>&1
+  rc=$?; echo "pmc clock $edge rc=$rc"
+  [ $rc -eq 0 ] || exit $rc
 done
 find $P -name '*.csv' | sort
