@@ -317,6 +317,8 @@ void oracle_to_pairs(uint32_t w0, uint32_t w1, uint32_t* e, uint32_t* o) {
 uint64_t oracle_hash_packed(const uint32_t* board, int64_t wwords, int64_t row0, int64_t rows,
                             int64_t pitch, int pairs) {
     uint64_t h = 0;
+    /* a sum mod 2^64 commutes: rows in parallel give the same value */
+#pragma omp parallel for schedule(static) reduction(+ : h) if (rows * wwords > (1 << 20))
     for (int64_t r = 0; r < rows; ++r) {
         for (int64_t c = 0; c < wwords; ++c) {
             uint32_t word = board[r * pitch + c];
