@@ -100,14 +100,30 @@ struct Words {
 // Unconditional load (callers clamp the column into the row), so no
 // exec-masked branch separates a load from its use and the compiler's
 // counted vmcnt waits keep the prefetch ring in flight.
+#ifndef GOL_NT_LOADS
+#define GOL_NT_LOADS 0
+#endif
+#ifndef GOL_NT_STORES
+#define GOL_NT_STORES 0
+#endif
 template <int VEC>
 __device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VEC>& d) {
     if constexpr (VEC == 4) {
+#if GOL_NT_LOADS
+        const U32x4 v = __builtin_nontemporal_load(reinterpret_cast<const U32x4*>(rp + col));
+        d.w[0] = v[0]; d.w[1] = v[1]; d.w[2] = v[2]; d.w[3] = v[3];
+#else
         const uint4 v = *reinterpret_cast<const uint4*>(rp + col);
         d.w[0] = v.x; d.w[1] = v.y; d.w[2] = v.z; d.w[3] = v.w;
+#endif
     } else if constexpr (VEC == 2) {
+#if GOL_NT_LOADS
+        const U32x2 v = __builtin_nontemporal_load(reinterpret_cast<const U32x2*>(rp + col));
+        d.w[0] = v[0]; d.w[1] = v[1];
+#else
         const uint2 v = *reinterpret_cast<const uint2*>(rp + col);
         d.w[0] = v.x; d.w[1] = v.y;
+#endif
     } else {
         d.w[0] = rp[col];
     }
@@ -127,12 +143,12 @@ __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t ro
     const int voff = lane_ok ? col * 4 : 0x7FFFFFF0;
     if constexpr (VEC == 4) {
         const U32x4 v = {d.w[0], d.w[1], d.w[2], d.w[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, GOL_NT_STORES ? 2 : 0);
     } else if constexpr (VEC == 2) {
         const U32x2 v = {d.w[0], d.w[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, 0, GOL_NT_STORES ? 2 : 0);
     } else {
-        __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, GOL_NT_STORES ? 2 : 0);
     }
 }
 

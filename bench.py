@@ -182,15 +182,34 @@ def secondary_run(GolEngine, torch, dist, a, local):
         # generations, rounded up to whole 6-generation passes
         n2, w2 = max(a.steps, 102), max(a.warmup, 12)
         dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
-    r2 = roofline(kms2, l2, g2, S * S)
-    if r2 is not None:
-        t = pmc_traffic(f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
-        if t is not None:
-            r2["traffic"] = t.get("hbm_bytes_per_launch")
-            r2["traffic_source"] = t.get("source")
+        # the same board one generation per HBM pass: the pure bandwidth case
+        # (north_star: >= 70 % of peak HBM bandwidth at 65536^2)
+        e2.set_tuning(band_rows=a.band, gens_per_pass=1)
+        e2.seed(0x5EED)
+        dt1, kms1, l1, g1 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
+    r2 = with_traffic(roofline(kms2, l2, g2, S * S), f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
+    r1 = with_traffic(roofline(kms1, l1, g1, S * S), f"{S}x{S}/N1/G1")
     return {"workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
             "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": w2,
-            "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2}
+            "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2,
+            "single_generation_passes": {"value": round(S * S * n2 / dt1 / 1e9, 2), "unit": "GCUPS",
+                                         "ms_per_step": round(dt1 / n2 * 1e3, 4), "roofline": r1}}
+
+
+def with_traffic(r, key):
+    """Add the PMC-measured HBM bytes per launch (and the bandwidth they
+    imply at the measured launch time) to a roofline object."""
+    if r is None:
+        return None
+    t = pmc_traffic(key)
+    if t is not None:
+        r["traffic"] = t.get("hbm_bytes_per_launch")
+        r["traffic_source"] = t.get("source")
+        if r["traffic"]:
+            gbs = r["traffic"] / (r["avg_launch_ms"] * 1e-3) / 1e9
+            r["measured_hbm_gbs"] = round(gbs, 1)
+            r["measured_hbm_frac"] = round(gbs / HBM_PEAK_GBS, 4)
+    return r
 
 
 def main():
@@ -229,10 +248,7 @@ def main():
         if "multistep_hg_kernel<2," in roof["kernel"] and N.pair_layout(W):
             # per-launch rate of the dominant kernel, not the wall-clock value
             roof["valu"] = valu_roofline(cells * gcov / launches / (roof["avg_launch_ms"] * 1e-3) / 1e9)
-        t = pmc_traffic(key)
-        if t is not None:
-            roof["traffic"] = t.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = t.get("source")
+        with_traffic(roof, key)
     out = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 2),
