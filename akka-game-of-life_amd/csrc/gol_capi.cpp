@@ -281,7 +281,8 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
 // bulk.  Default: one resident round's worth of waves in bands of band / 3
 // (profiles/r01_tail_sweep.txt, reseeded boards, min of 4 rounds: +4 % on the
 // N = 8 per-rank shape 262144 x 32768, +2 % at x 65536, +1 % at x 131072 and
-// 262144^2, neutral at 65536^2).  GOL_TAIL="frac,div" overrides it (A/B
+// 262144^2; neutral to -3.6 % at 65536^2, so boards of < 32 strips keep one
+// band height).  GOL_TAIL="frac,div" overrides it (A/B
 // sweeps, scripts/tail_sweep.py); frac 0 disables it.
 struct TailSplit {
     int32_t rows = 0;  // rows at the end of the range in short bands (0: none)
@@ -301,7 +302,9 @@ TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int
         return {};  // a fixed band (tuning) is taken literally
     }
     TailSplit t;
-    if (frac <= 0.0 || div < 2 || resident <= 0 || strips <= 0) return t;
+    // narrow boards (< 32 strips, e.g. 65536^2 with 17) measured neutral to
+    // -3.6 % (profiles/r01_tail_sweep.txt, r01_band_sweep.txt): off unless forced
+    if (frac <= 0.0 || div < 2 || resident <= 0 || strips <= 0 || (!env && strips < 32)) return t;
     const int64_t waves = (rows + band - 1) / band * strips;
     if (waves <= resident) return t;  // a single round: nothing to even out
     const int b2 = std::max(8, band / div);
