@@ -291,7 +291,11 @@ __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (
 }
 
 // Hash term accumulation for one output row (DESIGN.md "State hash").
-template <int VEC>
+// lk2 holds (col + j) * K2, or -- EVENW: rows of an even number of words,
+// so the row's first global word index gb is even -- that plus the `| 1`
+// of an even product: (g K2) | 1 = g K2 + ((g & 1) ^ 1) for odd K2, and g has
+// the parity of col + j (hash_lane_k2).
+template <int VEC, bool EVENW>
 __device__ __forceinline__ void hash_row(const StepParams& p, int r, const uint32_t (&lk1)[VEC],
                                          const uint32_t (&lk2)[VEC], const Words<VEC>& o,
                                          unsigned long long& acc) {
@@ -300,9 +304,14 @@ __device__ __forceinline__ void hash_row(const StepParams& p, int r, const uint3
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
         const uint32_t k1 = rb1 + lk1[j];
-        const uint32_t k2 = (rb2 + lk2[j]) | 1u;
+        const uint32_t k2 = EVENW ? rb2 + lk2[j] : (rb2 + lk2[j]) | 1u;
         acc += (unsigned long long)(o.w[j] ^ k1) * (unsigned long long)k2;
     }
+}
+
+template <bool EVENW>
+__device__ __forceinline__ uint32_t hash_lane_k2(int c) {
+    return (uint32_t)c * kHashK2 + (EVENW ? (((uint32_t)c & 1u) ^ 1u) : 0u);
 }
 
 // wave reduce -> workgroup reduce -> one atomic per workgroup into a sharded slot
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = (uint32_t)(col + j) * kHashK2;
+            lk2[j] = hash_lane_k2<PAIRS>(col + j);
         }
         const bool up = (bandi & 1) != 0;
         // t-th stream row (t = 0 .. nrows+1) and i-th output row.
@@ -421,7 +430,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const int r = out_of(i);
             store_row<VEC>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
             if constexpr (HASH) {
-                if (in_band) hash_row<VEC>(p, r, lk1, lk2, o, acc);
+                if (in_band) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc);
             }
         };
 
@@ -486,7 +495,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
             lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = (uint32_t)(col + j) * kHashK2;
+            lk2[j] = hash_lane_k2<PAIRS>(col + j);
         }
         const bool up = (bandi & 1) != 0;
         // stream row m <-> local board row (the same for every stage)
@@ -538,7 +547,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                 if (s < G) {
                     st[s - 1][((u - s) % 3 + 3) % 3] = o;
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                        if (own_row) hash_row<VEC, PAIRS>(p, brow(m), lk1, lk2, o, acc[s - 1]);
                     }
                     // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
                     apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
@@ -547,7 +556,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        if (own_row) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc[G - 1]);
                     }
                 }
             }
@@ -702,7 +711,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
             cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
             lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = (uint32_t)(col + j) * kHashK2;
+            lk2[j] = hash_lane_k2<PAIRS>(col + j);
         }
         const bool up = (bandi & 1) != 0;
         auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
@@ -748,13 +757,13 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                 if (s < G) {
                     arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                        if (own_row) hash_row<VEC, PAIRS>(p, brow(m), lk1, lk2, o, acc[s - 1]);
                     }
                 } else {
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p, r, lk1, lk2, o, acc[G - 1]);
+                        if (own_row) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc[G - 1]);
                     }
                 }
             }

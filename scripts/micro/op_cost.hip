@@ -59,6 +59,9 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
             if constexpr (MODE == 38) asm volatile("v_add_u32_e32 %0, %1, %1" : "=v"(a[i]) : "v"(a[i]));
             if constexpr (MODE == 39) asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(a[i]) : "v"(a[i]), "v"(b[i]));
             if constexpr (MODE == 40) asm volatile("v_xor_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD" : "=v"(a[i]) : "v"(a[i]), "v"(b[i]));
+            if constexpr (MODE == 41) asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0" : "+v"(*(uint64_t*)&a[i & ~1]) : "v"(b[i]), "v"(c[i]) : "s40", "s41");
+            if constexpr (MODE == 42) OP2("v_mul_lo_u32");
+            if constexpr (MODE == 43) asm volatile("v_lshl_add_u64 %0, %1, 0, %0" : "+v"(*(uint64_t*)&a[i & ~1]) : "v"(*(uint64_t*)&b[i & ~1]));
             if constexpr (MODE == 17) asm volatile("v_pk_mov_b32 %0, %1, %2 op_sel:[0,1]" : "=v"(*(uint64_t*)&a[i & ~1]) : "v"(*(uint64_t*)&b[i & ~1]), "v"(*(uint64_t*)&c[i & ~1]));
         }
     }
@@ -136,5 +139,8 @@ int main() {
     run<14>("v_and_or_b32", out, clk, cus);
     run<15>("v_or3_b32", out, clk, cus);
     run<17>("v_pk_mov_b32", out, clk, cus);
+    run<41>("v_mad_u64_u32", out, clk, cus);
+    run<42>("v_mul_lo_u32", out, clk, cus);
+    run<43>("v_lshl_add_u64", out, clk, cus);
     return 0;
 }
