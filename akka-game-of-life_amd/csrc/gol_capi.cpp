@@ -188,7 +188,6 @@ EventPair* next_event_pair(gol_ctx* ctx) {
 
 // Automatic tuning (scripts/tune.py sweeps on MI355X, profiles/r01_*):
 // results never depend on these choices.
-constexpr int kAutoGensPerPass = 6;  // best depth at 65536^2 and 262144^2
 
 // Multi-generation kernel formulation (gol_stencil.h): 1 = vertical-first,
 // 2 = horizontal-first (default: ~13.5 instead of ~15.4 VALU per word and
@@ -557,16 +556,56 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
     return GOL_OK;
 }
 
-// Pass depth for the next `remaining` generations.  Every shard of a ring
-// must pick the same G (their halo messages must match), so a sharded pass
-// is capped by the smallest shard of the decomposition, floor(H / N).
-int pass_depth(const gol_ctx* ctx, uint32_t remaining) {
-    int G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : kAutoGensPerPass;
-    G = std::min<int>(G, gol::kMaxGensPerPass);
-    G = std::min<int64_t>(G, remaining);
+// Deepest pass the context may run.  Every shard of a ring must pick the
+// same depths (their halo messages must match), so a sharded pass is capped
+// by the smallest shard of the decomposition, floor(H / N).
+int depth_cap(const gol_ctx* ctx) {
+    int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : gol::kMaxGensPerPass;
+    G = std::min<int64_t>(G, gol::kMaxGensPerPass);
     if (ctx->nccl && ctx->nranks > 1) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
-    return std::max(G, 1);
+    return (int)std::max<int64_t>(G, 1);
+}
+
+// Pass planner (DESIGN.md section 4 "Pass planner").  Relative time of one
+// pass of G generations (G = 1..8, G = 6 -> 1) on the multi-generation
+// kernels, from scripts/depth_sweep.py (profiles/r01_depth_sweep.txt, two
+// boxes): up to G = 6 a pass costs about the same (the sweep over the plane
+// is HBM-bound), G = 7 and 8 cost more but less per generation on wide boards
+// (>= 32 column strips); narrow boards are best at 6.
+constexpr double kPassCostWide[gol::kMaxGensPerPass + 1] = {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.115, 1.293};
+constexpr double kPassCostNarrow[gol::kMaxGensPerPass + 1] = {0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00,
+                                                             1.189, 1.379};
+
+// Depths of the passes that advance `n` generations.  A fixed
+// gens_per_pass (tuning) is taken literally (the last pass shorter);
+// otherwise the plan minimises the summed pass cost (a DP over n, n <= 1024:
+// callers plan per chunk).  Deterministic in (width, height, N, n), so all
+// shards of a ring plan alike.
+std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n) {
+    const int cap = depth_cap(ctx);
+    std::vector<int> plan;
+    if (ctx->gens_per_pass > 0 || cap == 1) {
+        for (uint32_t g = 0; g < n; g += plan.back()) plan.push_back((int)std::min<uint32_t>(cap, n - g));
+        return plan;
+    }
+    const int sw = gol::strip_words(lane_words(ctx, 6), 6);
+    const bool wide = (ctx->wwords + sw - 1) / sw >= 32;
+    const double* cost = wide ? kPassCostWide : kPassCostNarrow;
+    std::vector<double> best(n + 1, 0.0);
+    std::vector<int> pick(n + 1, 1);
+    for (uint32_t k = 1; k <= n; ++k) {
+        best[k] = 1e300;
+        for (int G = 1; G <= cap && (uint32_t)G <= k; ++G) {
+            const double c = best[k - G] + cost[G];
+            if (c < best[k] - 1e-12) {
+                best[k] = c;
+                pick[k] = G;
+            }
+        }
+    }
+    for (uint32_t k = n; k > 0; k -= (uint32_t)pick[k]) plan.push_back(pick[k]);
+    return plan;
 }
 
 void destroy_impl(gol_ctx* c) {
@@ -789,22 +828,20 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (int rc = bind(ctx)) return rc;
     if (generations == 0) return GOL_OK;
+    constexpr uint32_t kChunk = 1024;
     if (!hashes_out) {
-        for (uint32_t g = 0; g < generations;) {
-            const int G = pass_depth(ctx, generations - g);
-            if (int rc = one_pass(ctx, G, nullptr)) return rc;
-            g += (uint32_t)G;
-        }
+        for (uint32_t g0 = 0; g0 < generations; g0 += kChunk)
+            for (const int G : plan_passes(ctx, std::min(kChunk, generations - g0)))
+                if (int rc = one_pass(ctx, G, nullptr)) return rc;
         return GOL_OK;
     }
-    constexpr uint32_t kChunk = 1024;
     for (uint32_t g0 = 0; g0 < generations; g0 += kChunk) {
         const uint32_t n = std::min(kChunk, generations - g0);
         if (int rc = ensure_slots(ctx, n)) return rc;
         const size_t per = (size_t)gol::kHashGenStride;
         HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, n * per * sizeof(unsigned long long), ctx->compute));
-        for (uint32_t g = 0; g < n;) {
-            const int G = pass_depth(ctx, n - g);
+        uint32_t g = 0;
+        for (const int G : plan_passes(ctx, n)) {
             if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
             g += (uint32_t)G;
         }
@@ -995,6 +1032,15 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     return GOL_OK;
 }
 
+int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t* depths, int32_t max, int32_t* count) {
+    if (!ctx || !count || (max > 0 && !depths)) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (generations > 1024) return set_err(ctx, GOL_EINVAL, "plans cover at most 1024 generations");
+    const std::vector<int> plan = plan_passes(ctx, generations);
+    for (size_t k = 0; k < plan.size() && (int32_t)k < max; ++k) depths[k] = plan[k];
+    *count = (int32_t)plan.size();
+    return GOL_OK;
+}
+
 int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, int32_t* strip_words) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (gens_per_pass < 1 || gens_per_pass > gol::kMaxGensPerPass)
@@ -1103,8 +1149,8 @@ int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
                 base.push_back(s->slots);
             }
         }
-        for (uint32_t done = 0; done < cnt;) {
-            const int G = pass_depth(g->shards[0], cnt - done);
+        uint32_t done = 0;
+        for (const int G : plan_passes(g->shards[0], cnt)) {
             std::vector<unsigned long long*> slots;
             for (unsigned long long* b : base) slots.push_back(b + done * per);
             if (int rc = group_pass(g, G, slots)) return rc;

@@ -125,18 +125,26 @@ def roofline(kms, launches, gens_covered, cells_per_gen_per_launch):
             "generations_per_launch": gpl, "algorithmic_bytes_per_launch": algo}
 
 
-def kernel_label(info, G):
-    """Name of the kernel instance a G-generation pass launches: the strip width
-    (gol_occupancy) gives the words per lane; multi-generation passes at 8-byte
-    lanes or narrower run the horizontal-first kernel (gol_capi.cpp kernel_variant)."""
-    waves, strip = info.get(G, (0, 0))
-    if G == 1:
+def kernel_label(info, depths):
+    """Name of the kernel instances the timed passes launch (depths: the pass
+    plan, gol_pass_plan): the strip width (gol_occupancy) gives the words per
+    lane; multi-generation passes at 8-byte lanes or narrower run the
+    horizontal-first kernel (gol_capi.cpp kernel_variant)."""
+    gs = sorted(set(depths)) or [1]
+    waves, strip = info.get(gs[-1], (0, 0))
+    if gs == [1]:
         vec = strip // 64 if strip else "VEC"
         return f"gol::dev::step_kernel<{vec},LIFE>"
     vec = strip // 62 if strip else 0
     name = "multistep_hg_kernel" if vec in (1, 2) and os.environ.get("GOL_STENCIL_VARIANT", "2") != "1" \
         else "multistep_kernel"
-    return f"gol::dev::{name}<{vec or 'VEC'},{G},LIFE> ({waves} waves/CU resident)"
+    return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE> ({waves} waves/CU resident)"
+
+
+def traffic_key(W, H, world, gpp, steps):
+    """profiles/pmc_traffic.json key: fixed depth G, or the automatic plan of
+    `steps` generations (scripts/prof_run.py runs the same plan)."""
+    return f"{W}x{H}/N{world}/G{gpp}" if gpp else f"{W}x{H}/N{world}/auto{steps}"
 
 
 # Issue-cost model of the multi-generation kernel (DESIGN.md "Roofline"):
@@ -187,7 +195,7 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.set_tuning(band_rows=a.band, gens_per_pass=1)
         e2.seed(0x5EED)
         dt1, kms1, l1, g1 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
-    r2 = with_traffic(roofline(kms2, l2, g2, S * S), f"{S}x{S}/N1/G{round(g2 / l2) if l2 else 1}")
+    r2 = with_traffic(roofline(kms2, l2, g2, S * S), traffic_key(S, S, 1, a.gpp, n2))
     r1 = with_traffic(roofline(kms1, l1, g1, S * S), f"{S}x{S}/N1/G1")
     return {"workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
             "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": w2,
@@ -236,15 +244,17 @@ def main():
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
     eng_info = {g: eng.occupancy(g) for g in range(1, 9)}
+    plan = eng.pass_plan(min(a.steps, 1024))
     value = W * H * a.steps / dt / 1e9
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
-    G = round(gcov / launches) if launches else (a.gpp or 1)
-    cells = W * (rows if world == 1 else max(rows - 2 * G, 0))
+    G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
+    cells = W * (rows if world == 1 else max(rows - round(2 * G), 0))
     roof = roofline(kms, launches, gcov, cells)
-    key = f"{W}x{H}/N{world}/G{G}"
+    key = traffic_key(W, H, world, a.gpp, a.steps)
     if roof is not None:
-        roof["kernel"] = kernel_label(eng_info, G)
+        roof["kernel"] = kernel_label(eng_info, plan)
+        roof["pass_plan"] = plan
         if "multistep_hg_kernel<2," in roof["kernel"] and N.pair_layout(W):
             # per-launch rate of the dominant kernel, not the wall-clock value
             roof["valu"] = valu_roofline(cells * gcov / launches / (roof["avg_launch_ms"] * 1e-3) / 1e9)
@@ -266,7 +276,7 @@ def main():
                                f"(BASELINE.json configs[3]; N=1 = whole board on one GPU)",
                    "board": [W, H], "rule": "B3/S23", "topology": "torus",
                    "parallelism": f"row-block x{world}, RCCL halo send/recv",
-                   "generations_per_pass": G, "band_rows": a.band or "auto",
+                   "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash)},
         "roofline": roof,
     }

@@ -197,10 +197,16 @@ int gol_profile_reset(gol_ctx* ctx);
  * choice, which is also the default of a new context:
  *   band_rows       rows of output streamed by one wave;
  *   gens_per_pass   generations fused per HBM pass (temporal blocking, 1..8;
- *                   automatic: 6, fewer when fewer generations remain);
+ *                   automatic: the pass planner, see gol_pass_plan);
  *   words_per_lane  32-bit words each lane owns per row (1, 2 or 4; must
  *                   divide the words of a row). */
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane);
+
+/* Diagnostic: the pass depths (generations fused per HBM pass) gol_step would
+ * use to advance `generations` generations (at most 1024: gol_step plans per
+ * chunk of 1024), in launch order.  Writes at most `max` depths to `depths`
+ * and their number to `count`. */
+int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t* depths, int32_t max, int32_t* count);
 
 /* Diagnostic: resident 64-lane waves per CU of the step kernel a pass of
  * `gens_per_pass` generations would launch with the context's current

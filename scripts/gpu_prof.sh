@@ -15,7 +15,8 @@ rc=$?; echo "bench rc=$rc"; cat $P/bench.json
 for edge in 262144 65536; do
   for g in 0 1; do
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -k 10 300 rocprofv3 --pmc $c -T -d $P/pmc_${c}_${edge}_g$g -o run --output-format csv -- python3 scripts/prof_run.py $edge 60 $g > $P/pmc_${c}_${edge}_g$g.log 2>&1
+      gens=60; [ $edge = 65536 ] && [ $g = 0 ] && gens=102  # bench.py's timed generations
+      timeout -k 10 300 rocprofv3 --pmc $c -T -d $P/pmc_${c}_${edge}_g$g -o run --output-format csv -- python3 scripts/prof_run.py $edge $gens $g > $P/pmc_${c}_${edge}_g$g.log 2>&1
       rc=$?; echo "pmc $c $edge g$g rc=$rc"
       [ $rc -eq 0 ] || exit $rc
     done
@@ -23,7 +24,7 @@ for edge in 262144 65536; do
 done
 for edge in 262144 65536; do
   timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-    -T -d $P/pmc_clock_$edge -o run --output-format csv -- python3 scripts/prof_run.py $edge 60 0 > $P/pmc_clock_$edge.log 2>&1
+    -T -d $P/pmc_clock_$edge -o run --output-format csv -- python3 scripts/prof_run.py $edge 60 6 > $P/pmc_clock_$edge.log 2>&1
   rc=$?; echo "pmc clock $edge rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done

@@ -2,7 +2,7 @@
 """Effective clock and VALU issue of the step kernel from one rocprofv3 PMC
 pass (scripts/gpu_prof.sh: GRBM_GUI_ACTIVE, SQ_WAVES, SQ_INSTS_VALU,
 SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES over
-scripts/prof_run.py EDGE 60 0), per dispatch:
+scripts/prof_run.py EDGE 60 6: fixed 6-generation passes), per dispatch:
 
   clock            = GRBM_GUI_ACTIVE / 8 XCDs / kernel time   (MI355X_MICROARCH.md "DVFS")
   VALU/word-gen    = SQ_INSTS_VALU x 64 lanes / (32-bit words x generations)

@@ -24,6 +24,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = ("step_kernel", "multistep_kernel", "multistep_hg_kernel")
+GENS = {262144: 60, 65536: 102}  # timed generations of bench.py's two boards
 
 
 def rows(path):
@@ -84,24 +85,28 @@ def main():
                 continue
             fetch = pmc_per_dispatch(fdir, "FETCH_SIZE")
             write = pmc_per_dispatch(wdir, "WRITE_SIZE")
-            G = 6 if g == 0 else 1
-            # steady-state launches only (the last one may be a remainder pass)
+            # g = 0: the automatic pass plan of the bench's generation count
+            # (mixed depths: per-launch means), g = 1: single-generation passes
+            gens = GENS[edge] if g == 0 else 60
             n = min(len(fetch), len(write))
             fetch, write = fetch[:n], write[:n]
-            hbm = (2 * statistics.median(fetch) + statistics.median(write)) * 1024
-            algo = edge * edge * 0.25 * G
+            G = gens / n if g == 0 else 1  # generations per launch
+            f_b, w_b = 2 * statistics.fmean(fetch) * 1024, statistics.fmean(write) * 1024
+            hbm = f_b + w_b
             plane = edge * edge / 8
-            traffic[f"{edge}x{edge}/N1/G{G}"] = {
+            key = f"{edge}x{edge}/N1/auto{gens}" if g == 0 else f"{edge}x{edge}/N1/G1"
+            traffic[key] = {
                 "hbm_bytes_per_launch": round(hbm),
-                "fetch_bytes_per_launch": round(2 * statistics.median(fetch) * 1024),
-                "write_bytes_per_launch": round(statistics.median(write) * 1024),
-                "planes_read": round(2 * statistics.median(fetch) * 1024 / plane, 3),
-                "planes_written": round(statistics.median(write) * 1024 / plane, 3),
-                "algorithmic_bytes_per_launch": algo,
+                "fetch_bytes_per_launch": round(f_b),
+                "write_bytes_per_launch": round(w_b),
+                "planes_read": round(f_b / plane, 3),
+                "planes_written": round(w_b / plane, 3),
+                "generations_per_launch": round(G, 3),
+                "algorithmic_bytes_per_launch": edge * edge * 0.25 * G,
                 "hbm_bytes_per_cell_generation": round(hbm / (edge * edge * G), 4),
                 "launches_measured": n,
                 "source": f"profiles/{tag}_pmc (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                          f"scripts/prof_run.py {edge} 60 {g}; FETCH_SIZE x2 gfx950 correction)"}
+                          f"scripts/prof_run.py {edge} {gens} {g}; FETCH_SIZE x2 gfx950 correction)"}
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     pdir = os.path.join(dst, f"{tag}_pmc")

@@ -276,3 +276,27 @@ def test_known_patterns_on_gpu(gpu):
         assert (O.unpack(e.snapshot(), W) == shifted).all()
         e.step(4 * 64 - 4)
         assert (O.unpack(e.snapshot(), W) == cells).all()
+
+
+def test_pass_plan(gpu):
+    """gol_pass_plan: the depths cover the generations exactly, respect the
+    cap (8, or a fixed gens_per_pass), and wide boards fuse deeper passes
+    (DESIGN.md "Pass planner")."""
+    with engine(32 * 300, 64) as e:  # narrow: 6-generation passes
+        for n in (1, 5, 6, 7, 13, 50, 60, 1024):
+            plan = e.pass_plan(n)
+            assert sum(plan) == n and all(1 <= g <= 8 for g in plan), (n, plan)
+        assert e.pass_plan(60) == [6] * 10
+        e.set_tuning(gens_per_pass=4)
+        assert e.pass_plan(10) == [4, 4, 2]
+    with engine(262144, 64) as e:  # wide (67 strips): 7- and 8-generation passes
+        plan = e.pass_plan(60)
+        assert sum(plan) == 60 and set(plan) <= {7, 8}, plan
+        check = e.pass_plan(13)
+        assert sum(check) == 13
+    with engine(32 * 64, 21) as e:  # the plan's passes step bit-exactly
+        board = O.seed_packed(32 * 64, 21, 4)
+        e.load(board)
+        got = e.step(50, hashes=True)
+        _, want = O.run_packed(board, 32 * 64, 50, O.TORUS, O.LIFE)
+        np.testing.assert_array_equal(got, want)
