@@ -573,16 +573,21 @@ int depth_cap(const gol_ctx* ctx) {
 // boxes): up to G = 6 a pass costs about the same (the sweep over the plane
 // is HBM-bound), G = 7 and 8 cost more but less per generation on wide boards
 // (>= 32 column strips); narrow boards are best at 6.
-constexpr double kPassCostWide[gol::kMaxGensPerPass + 1] = {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.115, 1.293};
-constexpr double kPassCostNarrow[gol::kMaxGensPerPass + 1] = {0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00,
-                                                             1.189, 1.379};
+// With the fused per-generation hash the kernels are VALU-bound from G = 5
+// on, and 5 or 6 is best everywhere (HASH=1 rows of the same sweep).
+constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
+    // [hashed][wide]
+    {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.189, 1.379},     // narrow
+     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.115, 1.293}},       // wide
+    {{0, 0.572, 0.664, 0.682, 0.715, 0.834, 1.00, 1.248, 1.530},     // narrow, hashed
+     {0, 0.581, 0.772, 0.784, 0.771, 0.829, 1.00, 1.178, 1.410}}};   // wide, hashed
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);
 // otherwise the plan minimises the summed pass cost (a DP over n, n <= 1024:
 // callers plan per chunk).  Deterministic in (width, height, N, n), so all
 // shards of a ring plan alike.
-std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n) {
+std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n, bool hashed) {
     const int cap = depth_cap(ctx);
     std::vector<int> plan;
     if (ctx->gens_per_pass > 0 || cap == 1) {
@@ -591,7 +596,7 @@ std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n) {
     }
     const int sw = gol::strip_words(lane_words(ctx, 6), 6);
     const bool wide = (ctx->wwords + sw - 1) / sw >= 32;
-    const double* cost = wide ? kPassCostWide : kPassCostNarrow;
+    const double* cost = kPassCost[hashed ? 1 : 0][wide ? 1 : 0];
     std::vector<double> best(n + 1, 0.0);
     std::vector<int> pick(n + 1, 1);
     for (uint32_t k = 1; k <= n; ++k) {
@@ -831,7 +836,7 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
     constexpr uint32_t kChunk = 1024;
     if (!hashes_out) {
         for (uint32_t g0 = 0; g0 < generations; g0 += kChunk)
-            for (const int G : plan_passes(ctx, std::min(kChunk, generations - g0)))
+            for (const int G : plan_passes(ctx, std::min(kChunk, generations - g0), false))
                 if (int rc = one_pass(ctx, G, nullptr)) return rc;
         return GOL_OK;
     }
@@ -841,7 +846,7 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
         const size_t per = (size_t)gol::kHashGenStride;
         HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, n * per * sizeof(unsigned long long), ctx->compute));
         uint32_t g = 0;
-        for (const int G : plan_passes(ctx, n)) {
+        for (const int G : plan_passes(ctx, n, true)) {
             if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
             g += (uint32_t)G;
         }
@@ -1032,10 +1037,11 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     return GOL_OK;
 }
 
-int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t* depths, int32_t max, int32_t* count) {
+int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t with_hashes, int32_t* depths, int32_t max,
+                  int32_t* count) {
     if (!ctx || !count || (max > 0 && !depths)) return set_err(ctx, GOL_EINVAL, "null argument");
     if (generations > 1024) return set_err(ctx, GOL_EINVAL, "plans cover at most 1024 generations");
-    const std::vector<int> plan = plan_passes(ctx, generations);
+    const std::vector<int> plan = plan_passes(ctx, generations, with_hashes != 0);
     for (size_t k = 0; k < plan.size() && (int32_t)k < max; ++k) depths[k] = plan[k];
     *count = (int32_t)plan.size();
     return GOL_OK;
@@ -1150,7 +1156,7 @@ int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
             }
         }
         uint32_t done = 0;
-        for (const int G : plan_passes(g->shards[0], cnt)) {
+        for (const int G : plan_passes(g->shards[0], cnt, hashes_out != nullptr)) {
             std::vector<unsigned long long*> slots;
             for (unsigned long long* b : base) slots.push_back(b + done * per);
             if (int rc = group_pass(g, G, slots)) return rc;

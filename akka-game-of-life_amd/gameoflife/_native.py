@@ -89,7 +89,7 @@ _SIGNATURES = {
     "gol_set_tuning": (_c.c_int, [_vp, _c.c_int32, _c.c_int32, _c.c_int32]),
     "gol_selftest": (_c.c_int, [_c.c_int, _u32p]),
     "gol_occupancy": (_c.c_int, [_vp, _c.c_int32, ctypes.POINTER(_c.c_int32), ctypes.POINTER(_c.c_int32)]),
-    "gol_pass_plan": (_c.c_int, [_vp, _c.c_uint32, ctypes.POINTER(_c.c_int32), _c.c_int32,
+    "gol_pass_plan": (_c.c_int, [_vp, _c.c_uint32, _c.c_int32, ctypes.POINTER(_c.c_int32), _c.c_int32,
                                  ctypes.POINTER(_c.c_int32)]),
     "gol_group_create": (_c.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c.c_int]),
     "gol_group_step": (_c.c_int, [_vp, _c.c_uint32, _u64p]),

@@ -145,11 +145,11 @@ class GolEngine:
         self._chk(N.lib.gol_occupancy(self._h, gens_per_pass, ctypes.byref(w), ctypes.byref(s)))
         return w.value, s.value
 
-    def pass_plan(self, generations: int) -> list[int]:
+    def pass_plan(self, generations: int, hashes: bool = False) -> list[int]:
         """Pass depths gol_step would use for `generations` (<= 1024) generations."""
         buf = (ctypes.c_int32 * max(generations, 1))()
         n = ctypes.c_int32(0)
-        self._chk(N.lib.gol_pass_plan(self._h, generations, buf, len(buf), ctypes.byref(n)))
+        self._chk(N.lib.gol_pass_plan(self._h, generations, int(hashes), buf, len(buf), ctypes.byref(n)))
         return list(buf[:n.value])
 
     def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0, words_per_lane: int = 0) -> None:

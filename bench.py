@@ -244,7 +244,7 @@ def main():
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
     eng_info = {g: eng.occupancy(g) for g in range(1, 9)}
-    plan = eng.pass_plan(min(a.steps, 1024))
+    plan = eng.pass_plan(min(a.steps, 1024), hashes=a.hash)
     value = W * H * a.steps / dt / 1e9
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)

@@ -204,9 +204,10 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
 
 /* Diagnostic: the pass depths (generations fused per HBM pass) gol_step would
  * use to advance `generations` generations (at most 1024: gol_step plans per
- * chunk of 1024), in launch order.  Writes at most `max` depths to `depths`
- * and their number to `count`. */
-int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t* depths, int32_t max, int32_t* count);
+ * chunk of 1024) with or without per-generation hashes, in launch order.
+ * Writes at most `max` depths to `depths` and their number to `count`. */
+int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t with_hashes, int32_t* depths, int32_t max,
+                  int32_t* count);
 
 /* Diagnostic: resident 64-lane waves per CU of the step kernel a pass of
  * `gens_per_pass` generations would launch with the context's current

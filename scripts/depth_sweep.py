@@ -3,7 +3,7 @@
 6 warm-up generations, 24 timed generations, min of ROUNDS interleaved rounds):
 the cost table behind gol_step's pass planner.
 
-    python scripts/depth_sweep.py [WxH ...]     env: ROUNDS=3
+    python scripts/depth_sweep.py [WxH ...]     env: ROUNDS=3  HASH=1 (fused hashes)
 """
 import os
 import sys
@@ -18,6 +18,7 @@ def main():
     shapes = [tuple(int(x) for x in (a.split("x") if "x" in a else (a, a))) for a in sys.argv[1:]] or \
         [(262144, 262144), (262144, 32768), (65536, 65536)]
     rounds = int(os.environ.get("ROUNDS", "3"))
+    hashes = os.environ.get("HASH", "0") == "1"
     for W, H in shapes:
         with GolEngine(W, H) as e:
             res = {}
@@ -29,7 +30,7 @@ def main():
                     e.step(6)
                     e.profile(True)
                     e.profile_reset()
-                    e.step(gens)
+                    e.step(gens, hashes=hashes)
                     e.sync()
                     ms, n, g = e.profile_read()
                     e.profile(False)
@@ -37,7 +38,7 @@ def main():
             base = min(res[6])
             for G in range(1, 9):
                 t = min(res[G])
-                print(f"shape={W}x{H} G={G} ms/pass={t:.4f} ms/gen={t / G:.4f} pass/pass(G=6)={t / base:.3f} "
+                print(f"shape={W}x{H} hash={int(hashes)} G={G} ms/pass={t:.4f} ms/gen={t / G:.4f} pass/pass(G=6)={t / base:.3f} "
                       f"GCUPS={W * H * G / t / 1e6:9.1f}", flush=True)
 
 

@@ -292,6 +292,8 @@ def test_pass_plan(gpu):
     with engine(262144, 64) as e:  # wide (67 strips): 7- and 8-generation passes
         plan = e.pass_plan(60)
         assert sum(plan) == 60 and set(plan) <= {7, 8}, plan
+        hplan = e.pass_plan(60, hashes=True)  # hashed passes are VALU-bound: 5 or 6
+        assert sum(hplan) == 60 and set(hplan) <= {5, 6}, hplan
         check = e.pass_plan(13)
         assert sum(check) == 13
     with engine(32 * 64, 21) as e:  # the plan's passes step bit-exactly
