@@ -164,16 +164,21 @@ __device__ __forceinline__ WaveTile wave_tile(const StepParams& p, int wave) {
     return {range, w % p.strips, w / p.strips};
 }
 
-// Local row pointer for r in [-G, rows + G).
+// Local row pointer for r in [-G, rows + G).  Wave-uniform and built from
+// selects rather than branches: it runs once per stream row inside the
+// unrolled loops.  Only tori shorter than a pass's halo (rows < G) take the
+// one uniform branch, to wrap more than once.
 __device__ __forceinline__ const uint32_t* row_ptr(const StepParams& p, int r, int G) {
-    if (p.wrap_y) {
-        while (r < 0) r += p.rows;
-        while (r >= p.rows) r -= p.rows;
-        return p.cur + (int64_t)r * p.pitch;
+    const bool top = r < 0, bot = r >= p.rows;
+    int w = top ? r + p.rows : (bot ? r - p.rows : r);  // torus: one wrap
+    if (p.wrap_y && p.rows < G) {
+        w = r % p.rows;
+        w = w < 0 ? w + p.rows : w;
     }
-    if (r < 0) return p.halo_top + (int64_t)(r + G) * p.halo_stride;
-    if (r >= p.rows) return p.halo_bot + (int64_t)(r - p.rows) * p.halo_stride;
-    return p.cur + (int64_t)r * p.pitch;
+    const bool halo = !p.wrap_y && (top || bot);
+    const uint32_t* base = halo ? (top ? p.halo_top : p.halo_bot) : p.cur;
+    const int64_t idx = halo ? (top ? r + G : r - p.rows) : (p.wrap_y ? w : r);
+    return base + idx * (halo ? p.halo_stride : p.pitch);
 }
 
 template <bool CLIPPED>
