@@ -45,8 +45,13 @@ namespace dev {
 
 constexpr int kPF = 2;               // step_kernel: rows prefetched ahead
 constexpr int kRing = kPF + 3;       // step_kernel: register ring of stream rows
+constexpr int kMRing = 6;            // multistep kernels: input ring (multiple of 3)
 constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
-constexpr int kMRing = 6;            // multistep_kernel: input ring (multiple of 3)
+#ifndef GOL_HG_PF
+#define GOL_HG_PF 2
+#endif
+constexpr int kHgPF = GOL_HG_PF;     // multistep_hg_kernel: rows prefetched ahead (< kMRing)
+static_assert(kHgPF >= 1 && kHgPF < kMRing, "prefetch slots");
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
 
@@ -199,6 +204,33 @@ constexpr uint32_t kAAndBOrC = 0xE0;     // a & (b | c)
 
 #define GOL_BITOP3(a, b, c, imm) __builtin_amdgcn_bitop3_b32((a), (b), (c), (imm))
 
+// Full-sum B3/S23 circuit (rule_b3s23_fullsum).  Truth tables index bit (a << 2 | b << 1 | c).
+constexpr uint32_t kXnor3 = 0x69;      // ~(a ^ b ^ c): the plane's 3-sum is 0 or 2
+constexpr uint32_t kNotAllEq = 0x7E;   // the plane's 3-sum is 1 or 2
+constexpr uint32_t kRuleT1 = 0x56;
+constexpr uint32_t kRuleT2 = 0x45;
+constexpr uint32_t kRuleOut = 0x28;    // (a ^ b) & c
+
+// B3/S23 from the full 9-cell sum S = a + c + b of three 2-bit terms (row or
+// column 3-sums, bit planes x0/x1): alive next iff S == 3 or (S == 4 and the
+// centre is alive).  Per bit plane one "sum is even" and one "terms not all
+// equal" bitop3, then a 3-gate tail: 7 v_bitop3, where the centre-less count
+// (n = S - centre, then ~qq & (pp ^ c0) & (n0 | alive)) takes 7 + the
+// centre's removal.  Found by exhaustive search over 3-gate circuits on
+// symmetric plane encodings (DESIGN.md §4 "Rule circuit"), checked on every
+// input by tests/test_rule_circuit.py.  Only for tori: on clipped boards the
+// visible centre (summed) and the alive centre differ at the sink cells.
+__device__ __forceinline__ uint32_t rule_b3s23_fullsum(uint32_t a0, uint32_t a1, uint32_t c0, uint32_t c1,
+                                                       uint32_t b0, uint32_t b1, uint32_t alive) {
+    const uint32_t e1 = GOL_BITOP3(a0, c0, b0, kXnor3);
+    const uint32_t e2 = GOL_BITOP3(a0, c0, b0, kNotAllEq);
+    const uint32_t f1 = GOL_BITOP3(a1, c1, b1, kXnor3);
+    const uint32_t f2 = GOL_BITOP3(a1, c1, b1, kNotAllEq);
+    const uint32_t t1 = GOL_BITOP3(e1, e2, f2, kRuleT1);
+    const uint32_t t2 = GOL_BITOP3(e1, alive, t1, kRuleT2);
+    return GOL_BITOP3(e2, f1, t2, kRuleOut);
+}
+
 // Column sums of the visible rows: (v1 v0) = a + c + b (the full 3-cell
 // column, seen by the columns left and right of it) and (p1 p0) = a + b (the
 // column minus its centre, seen by the centre cell itself).
@@ -238,7 +270,7 @@ __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC
 // in is the previous pair's last odd column) and column x+1 is the odd word
 // itself; mirror-wise for odd-column words.  One funnel shift per word
 // instead of two (v_alignbit issues at half the rate of v_bitop3 on gfx950).
-template <int VEC, bool LIFE, bool PAIRS>
+template <int VEC, bool LIFE, bool PAIRS, bool CLIPPED>
 __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (&v0)[VEC],
                                            const uint32_t (&v1)[VEC], const uint32_t (&p0)[VEC],
                                            const uint32_t (&p1)[VEC], uint32_t m0, uint32_t m1, uint32_t n0,
@@ -266,6 +298,12 @@ __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (
             w1 = l1;
             e0 = __builtin_amdgcn_alignbit(r0, l0, 1);
             e1 = __builtin_amdgcn_alignbit(r1, l1, 1);
+        }
+        if constexpr (LIFE && !CLIPPED) {
+            // full 9-cell sum S = v(x-1) + v(x) + v(x+1): the gate circuit of
+            // rule_hg (rule_b3s23_fullsum); the centre-less pair p is unused
+            out.w[j] = rule_b3s23_fullsum(w0, w1, v0[j], v1[j], e0, e1, alive.w[j]);
+            continue;
         }
         const uint32_t nb0 = GOL_BITOP3(w0, e0, p0[j], kXor3);
         const uint32_t c0 = GOL_BITOP3(w0, e0, p0[j], kMaj);
@@ -427,7 +465,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 n1 = last ? r1 : n1;
             }
             Words<VEC> o;
-            rule_words<VEC, LIFE, PAIRS>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
+            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -531,7 +569,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             const uint32_t m1 = dpp_shr1_zero(v1[VEC - 1]);
             const uint32_t n0 = dpp_shl1_zero(v0[0]);
             const uint32_t n1 = dpp_shl1_zero(v1[0]);
-            rule_words<VEC, LIFE, PAIRS>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
+            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -647,6 +685,12 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
                                         const uint32_t (&omask)[VEC], Words<VEC>& out) {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
+        if constexpr (LIFE && !CLIPPED) {
+            // S = h(m-1) + h(m) + h(m+1): 7 v_bitop3 instead of g = h - r
+            // (1 v_xor + 1 v_bitop3) and the centre-less count's 6
+            out.w[j] = rule_b3s23_fullsum(A.h0[j], A.h1[j], C.h0[j], C.h1[j], B.h0[j], B.h1[j], C.r[j]);
+            continue;
+        }
         const uint32_t g0 = C.h0[j] ^ C.r[j];
         const uint32_t g1 = GOL_BITOP3(C.h1[j], C.h0[j], C.r[j], kAndOrNotC);
         const uint32_t nb0 = GOL_BITOP3(A.h0[j], B.h0[j], g0, kXor3);
@@ -740,14 +784,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 
         auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
 
-        // Stream row q (ring slot u = q % kMRing): prefetch row q + kMPF,
+        // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF,
         // input row q arrives at ring 0, stage s produces stream row q - s.
         // Stage s has valid inputs only from q = 2s on (its rows m < s are
         // built from the clamped rows before the band and are never stored,
         // hashed or read by a valid row), so the pipeline fill -- the first
         // kFill rows, q known at compile time -- skips those stage steps.
         auto row_step = [&](const int q, const int u, const bool fill) {
-            load_m(min(q + kMPF, n_in - 1), in[(u + kMPF) % kMRing]);
+            load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
             arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
             for (int s = 1; s <= G; ++s) {
@@ -775,7 +819,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
         };
 
 #pragma unroll
-        for (int t = 0; t < kMPF; ++t) load_m(min(t, n_in - 1), in[t]);
+        for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
         constexpr int kFill = (2 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
         // The peeled fill is one long straight-line block; only the B3/S23
         // instances keep their rings in registers through it (the generic-rule

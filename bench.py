@@ -151,7 +151,10 @@ def traffic_key(W, H, world, gpp, steps):
 # VALU instructions per 32-cell word and generation in the loop of
 # multistep_hg_kernel<2, G, LIFE> on the pair layout (from its ISA), and the
 # measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
-VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_xor_b32": (1, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
+# per 32-cell word and generation in the hg kernel's loop (full-sum rule circuit,
+# scripts/isa_loop.py census: 800 VALU per 6-row unroll at G = 6 = 72 DPP + 72
+# alignbit + 648 bitop3 + loop overhead), issue costs from op_cost.hip
+VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
 SIMDS = 256 * 4
 CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md max clock
 
