@@ -193,12 +193,25 @@ EventPair* next_event_pair(gol_ctx* ctx) {
 // 2 = horizontal-first (default: ~13.5 instead of ~15.4 VALU per word and
 // generation; +9 % at 262144^2, +24 % at 65536^2, profiles/r01_variant_ab.txt).
 // GOL_STENCIL_VARIANT overrides (A/B experiments).
+constexpr int kDefaultXcdChunk = 8;
+
 int stencil_variant() {
     static const int v = [] {
         const char* e = getenv("GOL_STENCIL_VARIANT");
         return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 2;
     }();
     return v;
+}
+
+// Blocks per XCD chunk of the step kernels' block order (gol_stencil.h
+// xcd_block).  GOL_XCD_CHUNK overrides (A/B experiments; 1 = dispatch order).
+int xcd_chunk() {
+    static const int c = [] {
+        const char* e = getenv("GOL_XCD_CHUNK");
+        const int v = e ? atoi(e) : kDefaultXcdChunk;
+        return v < 1 ? 1 : (v > 64 ? 64 : v);
+    }();
+    return c;
 }
 
 // Kernel formulation a pass at `vec` words per lane actually runs: 16-byte
@@ -389,6 +402,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.birth = ctx->birth;
     p.survive = ctx->survive;
     p.variant = kernel_variant(vec);
+    p.xcd_chunk = xcd_chunk();
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
     if (ctx->prof && main_launch) {

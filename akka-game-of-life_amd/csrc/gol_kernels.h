@@ -46,6 +46,7 @@ struct StepParams {
     uint32_t birth;
     uint32_t survive;
     int32_t variant;           // multi-generation kernel: 1 vertical-first, 2 horizontal-first
+    int32_t xcd_chunk;         // consecutive blocks kept on one XCD (gol_stencil.h xcd_block; <= 1: off)
 };
 
 // Strip geometry of a launch: words covered per wave.

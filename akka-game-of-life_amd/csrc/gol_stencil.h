@@ -159,6 +159,22 @@ __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t ro
 
 // Wave -> (row range, column strip, band of the range): range 0's bands
 // come first, then range 1's (StepParams).  Wave-uniform.
+// XCD-aware block order.  The dispatcher places block b on XCD b % 8, and
+// the XCDs have separate L2s.  A strip's halo lanes make every wave-load of
+// a 62-output-lane strip straddle cache lines shared with the neighbouring
+// strips, so blocks of adjacent strips on different XCDs fetch those lines
+// twice.  Within each group of 8 * C dispatched blocks, XCD x runs logical
+// blocks x*C .. x*C + C - 1 (adjacent strips of one band); the logical order
+// -- band-major, tail bands last -- is kept at the granularity of a group.
+// Blocks past the last whole group keep their index.  Measured with
+// scripts/micro/band_stream.hip (DESIGN.md §4 "Memory operations").
+__device__ __forceinline__ int xcd_block(int b, int nblocks, int chunk) {
+    const int group = 8 * chunk;
+    if (chunk <= 1 || b >= nblocks / group * group) return b;
+    const int g = b / group, r = b - g * group;
+    return g * group + (r & 7) * chunk + (r >> 3);
+}
+
 struct WaveTile {
     int range, strip, band;
 };
@@ -381,7 +397,7 @@ template <int VEC, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc = 0;
 
@@ -507,7 +523,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
     constexpr int kOut = (kWaveLanes - 2) * VEC;  // output words per strip
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
@@ -729,7 +745,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
     constexpr int kOut = (kWaveLanes - 2) * VEC;
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const WaveTile tile = wave_tile(p, blockIdx.x * kWavesPerWG + wave_in_wg);
+    const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
