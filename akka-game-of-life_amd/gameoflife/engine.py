@@ -72,8 +72,14 @@ class GolEngine:
         assert a.shape[0] == self.rows and a.shape[1] >= self.wwords, a.shape
         self._chk(N.lib.gol_load(self._h, a.ctypes.data_as(N._u32p), a.shape[1]))
 
-    def snapshot(self) -> np.ndarray:
-        out = np.zeros((self.rows, self.wwords), dtype=np.uint32)
+    def snapshot(self, out: np.ndarray | None = None) -> np.ndarray:
+        """Current board, row-major host layout.  `out`: a caller-owned
+        (rows, wwords) uint32 C-contiguous buffer to fill -- reusing one (or a
+        pinned one) avoids first-touch page faults on every snapshot."""
+        if out is None:
+            out = np.zeros((self.rows, self.wwords), dtype=np.uint32)
+        elif out.dtype != np.uint32 or out.shape != (self.rows, self.wwords) or not out.flags.c_contiguous:
+            raise ValueError(f"snapshot buffer must be a C-contiguous uint32 array of shape {(self.rows, self.wwords)}")
         self._chk(N.lib.gol_snapshot(self._h, out.ctypes.data_as(N._u32p), self.wwords))
         return out
 

@@ -302,3 +302,23 @@ def test_pass_plan(gpu):
         got = e.step(50, hashes=True)
         _, want = O.run_packed(board, 32 * 64, 50, O.TORUS, O.LIFE)
         np.testing.assert_array_equal(got, want)
+
+
+def test_snapshot_into_caller_buffer(gpu):
+    """gol_snapshot into a caller-owned buffer (GolEngine.snapshot(out=...)):
+    same board as a fresh snapshot; a buffer of the wrong shape or dtype is
+    refused before the copy."""
+    W, H = 4096, 77
+    board = O.seed_packed(W, H, 5)
+    with engine(W, H, topology="torus", rule=rule_obj(O.LIFE)) as e:
+        e.load(board)
+        e.step(3)
+        fresh = e.snapshot()
+        buf = np.full(fresh.shape, 0xFFFFFFFF, dtype=np.uint32)
+        assert e.snapshot(out=buf) is buf
+        np.testing.assert_array_equal(buf, fresh)
+        np.testing.assert_array_equal(fresh, O.run_packed(board, W, 3)[0])
+        for bad in (np.zeros((H, W // 32 + 1), np.uint32), np.zeros((H, W // 32), np.int64),
+                    np.zeros((W // 32, H), np.uint32).T):
+            with pytest.raises(ValueError):
+                e.snapshot(out=bad)
