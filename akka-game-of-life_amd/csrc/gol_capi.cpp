@@ -137,6 +137,10 @@ int bind(gol_ctx* ctx) {
 
 int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     if (gens <= ctx->slots_gens) return GOL_OK;
+    // one allocation for a whole gol_step chunk (1024 generations, 4 MiB):
+    // a hipFree + hipMalloc between two hashed calls would synchronise the
+    // device inside the caller's step
+    gens = std::max<uint32_t>(gens, 1024);
     if (ctx->slots) HIP_CHECK(ctx, hipFree(ctx->slots));
     ctx->slots = nullptr;
     const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
@@ -797,6 +801,18 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
         hipEventCreateWithFlags(&ctx->ev_halo, hipEventDisableTiming) != hipSuccess) {
         set_err(ctx, GOL_EHIP, "stream/event creation failed");
         return fail(GOL_EHIP);
+    }
+    // Load every step kernel instance this context can launch, now: the HIP
+    // runtime loads a code object on the first use of one of its kernels, and
+    // each pass depth lives in its own code object (gol_step_g<G>.hip), so the
+    // first gol_step that plans a new depth would otherwise stall inside the
+    // caller's timed region.  The occupancy query of an instance loads it
+    // (and fills the cache launch_ranges reads).
+    {
+        const bool clipped = ctx->topology == GOL_REF_CLIPPED;
+        const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
+        for (int G = 1; G <= gol::kMaxGensPerPass; ++G)
+            for (int h = 0; h < 2; ++h) (void)resident_waves(ctx, lane_words(ctx, G), G, life, h != 0, clipped);
     }
     if (hipDeviceSynchronize() != hipSuccess) {
         set_err(ctx, GOL_EHIP, "hipDeviceSynchronize failed");
