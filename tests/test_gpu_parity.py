@@ -282,11 +282,13 @@ def test_pass_plan(gpu):
     """gol_pass_plan: the depths cover the generations exactly, respect the
     cap (8, or a fixed gens_per_pass), and wide boards fuse deeper passes
     (DESIGN.md "Pass planner")."""
-    with engine(32 * 300, 64) as e:  # narrow: 6-generation passes
+    with engine(32 * 300, 64) as e:  # narrow: 8-generation passes, 6 to fill the remainder
         for n in (1, 5, 6, 7, 13, 50, 60, 1024):
             plan = e.pass_plan(n)
             assert sum(plan) == n and all(1 <= g <= 8 for g in plan), (n, plan)
-        assert e.pass_plan(60) == [6] * 10
+        assert e.pass_plan(48) == [8] * 6
+        assert sorted(e.pass_plan(60)) == [6, 6] + [8] * 6
+        assert e.pass_plan(60, hashes=True) == [6] * 10  # hashed: VALU-bound, 6 is best
         e.set_tuning(gens_per_pass=4)
         assert e.pass_plan(10) == [4, 4, 2]
     with engine(262144, 64) as e:  # wide (67 strips): 7- and 8-generation passes
