@@ -29,13 +29,13 @@ sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CELL_UPDATE = 0.25
-DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's automatic choice (6, from scripts/tune.py)
+DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass_plan, DESIGN.md "Pass planner")
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults are whole 6-generation passes (the automatic pass depth)
+    # defaults: 60 timed generations = 4 x 7 + 4 x 8 passes at 262144^2 (the planner's choice)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
