@@ -596,7 +596,7 @@ int depth_cap(const gol_ctx* ctx) {
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
     // [hashed][wide]
     {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26},       // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
-     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.115, 1.293}},       // wide
+     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231}},       // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
     {{0, 0.572, 0.664, 0.682, 0.715, 0.834, 1.00, 1.248, 1.530},     // narrow, hashed
      {0, 0.581, 0.772, 0.784, 0.771, 0.829, 1.00, 1.178, 1.410}}};   // wide, hashed
 
