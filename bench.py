@@ -35,7 +35,7 @@ DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: 60 timed generations = 4 x 7 + 4 x 8 passes at 262144^2 (the planner's choice)
+    # defaults: 60 timed generations = 2 x 6 + 6 x 8 passes at 262144^2 (the planner's choice)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
