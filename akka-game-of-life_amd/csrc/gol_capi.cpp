@@ -126,8 +126,12 @@ int set_err(gol_ctx* ctx, int code, const char* fmt, ...) {
 int64_t group_min_rows(const gol_group* g);
 size_t group_size(const gol_group* g);
 
+// Any attached communicator runs the ring schedule, a 1-rank one included: its
+// up and down neighbours are the rank itself, so the torus halo rows go out
+// and come back through ncclSend / ncclRecv to self (the "self-ring" -- the
+// RCCL path exercised bit-exactly on a one-GPU box).
 bool sharded(const gol_ctx* c) {
-    return (c->nccl != nullptr && c->nranks > 1) || (c->group != nullptr && group_size(c->group) > 1);
+    return c->nccl != nullptr || (c->group != nullptr && group_size(c->group) > 1);
 }
 
 int bind(gol_ctx* ctx) {
@@ -485,9 +489,10 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
         const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
         NCCL_CHECK(ctx, ncclGroupStart());
-        // Issue order matters when up == down (2 ranks): per-peer FIFO matching
-        // pairs my last rows with the peer's top halo and my first rows with
-        // its bottom halo (gameoflife/shard.py HaloPlan mirrors this order).
+        // Issue order matters when up == down (2 ranks, or 1 rank sending to
+        // itself): per-peer FIFO matching pairs my last rows with the peer's
+        // top halo and my first rows with its bottom halo
+        // (gameoflife/shard.py HaloPlan mirrors this order).
         if (has_down)
             NCCL_CHECK(ctx, ncclSend(cur + (int64_t)(rows - G) * pitch, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
         if (has_up) NCCL_CHECK(ctx, ncclSend(cur, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
@@ -576,11 +581,12 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
 
 // Deepest pass the context may run.  Every shard of a ring must pick the
 // same depths (their halo messages must match), so a sharded pass is capped
-// by the smallest shard of the decomposition, floor(H / N).
+// by the smallest shard of the decomposition, floor(H / N) (a 1-rank ring
+// sends G of its own rows: G <= H).
 int depth_cap(const gol_ctx* ctx) {
     int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : gol::kMaxGensPerPass;
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
-    if (ctx->nccl && ctx->nranks > 1) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
+    if (ctx->nccl) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return (int)std::max<int64_t>(G, 1);
 }
@@ -886,6 +892,14 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
         fold_slots(ctx, n, hashes_out + g0);
     }
     return GOL_OK;
+}
+
+int gol_step_ex(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out, size_t hashes_capacity) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (hashes_out && hashes_capacity < generations)
+        return set_err(ctx, GOL_EINVAL, "hashes_out holds %zu entries, %u generations requested", hashes_capacity,
+                       generations);
+    return gol_step(ctx, generations, hashes_out);
 }
 
 int gol_epoch(const gol_ctx* ctx, uint64_t* epoch) {

@@ -72,6 +72,7 @@ _SIGNATURES = {
     "gol_seed": (_c.c_int, [_vp, _c.c_uint64]),
     "gol_load": (_c.c_int, [_vp, _u32p, _c.c_int64]),
     "gol_step": (_c.c_int, [_vp, _c.c_uint32, _u64p]),
+    "gol_step_ex": (_c.c_int, [_vp, _c.c_uint32, _u64p, _c.c_size_t]),
     "gol_epoch": (_c.c_int, [_vp, _u64p]),
     "gol_sync": (_c.c_int, [_vp]),
     "gol_hash": (_c.c_int, [_vp, _u64p]),

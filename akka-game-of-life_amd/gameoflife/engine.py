@@ -87,7 +87,7 @@ class GolEngine:
         """Advance; returns the per-generation partial hashes (uint64) if asked."""
         if hashes:
             out = np.zeros(generations, dtype=np.uint64)
-            self._chk(N.lib.gol_step(self._h, generations, out.ctypes.data_as(N._u64p)))
+            self._chk(N.lib.gol_step_ex(self._h, generations, out.ctypes.data_as(N._u64p), out.size))
             return out
         self._chk(N.lib.gol_step(self._h, generations, None))
         return None

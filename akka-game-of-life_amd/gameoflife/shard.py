@@ -3,10 +3,13 @@
 The reference scales by adding backend JVMs and deploying cell actors on a
 random node (BoardCreator.scala:33-36,65-70); neighbours then talk across the
 network (application.conf:11-17).  Here rank r of n owns the contiguous row
-block ``gol_shard_rows(H, r, n)`` and exchanges one halo row with each ring
-neighbour per generation over RCCL (inside libgol).  This module holds the
-host-side pieces: the halo plan (the exact op order libgol issues, shared with
-the CPU tests), the hash reduction and the per-process backend worker.
+block ``gol_shard_rows(H, r, n)``.  Before every pass of G generations it
+exchanges G halo rows with each ring neighbour over RCCL (inside libgol,
+gol_capi.cpp one_pass): its first G rows go up, its last G rows go down, and
+G-row halos come back.  This module holds the host-side pieces: the halo plan
+(the exact op order and message shapes libgol issues, shared with the CPU
+tests), the pass-depth cap, the hash reduction and the per-process backend
+worker.
 """
 from __future__ import annotations
 
@@ -24,13 +27,37 @@ def shard_rows_py(height: int, rank: int, nranks: int) -> tuple[int, int]:
     return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
 
+MAX_GENS_PER_PASS = 8  # gol_kernels.h kMaxGensPerPass
+
+
+def ring_depth_cap(height: int, nranks: int, gens_per_pass: int = 0) -> int:
+    """Deepest pass a ring may run (gol_capi.cpp depth_cap): every rank must
+    issue identical halo messages, so the depth is capped by the smallest
+    shard, floor(H / N) rows (a 1-rank self-ring: H)."""
+    g = gens_per_pass if gens_per_pass > 0 else MAX_GENS_PER_PASS
+    return max(1, min(g, MAX_GENS_PER_PASS, height // nranks))
+
+
+def fixed_depth_plan(generations: int, depth: int) -> list[int]:
+    """Pass depths of a fixed gens_per_pass (gol_capi.cpp plan_passes: taken
+    literally, the last pass shorter)."""
+    plan, done = [], 0
+    while done < generations:
+        plan.append(min(depth, generations - done))
+        done += plan[-1]
+    return plan
+
+
 @dataclasses.dataclass(frozen=True)
 class HaloPlan:
-    """Per-generation halo exchange of one rank (gol_capi.cpp one_generation).
+    """Halo exchange of one rank before each pass (gol_capi.cpp one_pass).
 
-    ops are issued inside one group in this order; with 2 ranks up == down and
-    per-peer FIFO matching pairs the sender's last row with the receiver's top
-    halo and its first row with the bottom halo."""
+    A pass of G generations sends the rank's last G rows down and its first G
+    rows up, and receives the G rows above it (top halo) and below it (bottom
+    halo).  ops are issued inside one group in this order; with 2 ranks (or 1,
+    the self-ring) up == down and per-peer FIFO matching pairs the sender's
+    last rows with the receiver's top halo and its first rows with the bottom
+    halo."""
     rank: int
     nranks: int
     torus: bool

@@ -125,10 +125,18 @@ int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words);
  * (CellActor.scala:63-91, NextStateCellGathererActor.scala:25-48), for every
  * cell of the shard at once.  If hashes_out is not NULL it receives, for each
  * generation, the shard's partial state hash (DESIGN.md "State hash"); the
- * global hash is the sum mod 2^64 of the shards' partials.  With a
- * communicator attached, halo rows are exchanged over RCCL every generation.
- * Asynchronous when hashes_out is NULL (call gol_sync to wait). */
+ * global hash is the sum mod 2^64 of the shards' partials; hashes_out must
+ * hold `generations` entries (gol_step_ex checks a capacity).  With a
+ * communicator attached, G halo rows are exchanged over RCCL before every pass
+ * of G generations.  Asynchronous when hashes_out is NULL (call gol_sync to
+ * wait). */
 int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out);
+
+/* gol_step with the capacity of hashes_out (entries): GOL_EINVAL, and no
+ * generation advanced, when hashes_out is not NULL and holds fewer than
+ * `generations` entries.  The form a JVM binding calls with a direct buffer's
+ * capacity. */
+int gol_step_ex(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out, size_t hashes_capacity);
 
 /* Current epoch (CellActor.scala:39 myCurrentEpoch). */
 int gol_epoch(const gol_ctx* ctx, uint64_t* epoch);
@@ -160,7 +168,10 @@ int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes);
 /* Multi-GPU: RCCL communicator over the ring of row-block shards.  Replaces
  * the cross-backend neighbour messages (GetStateFromEpoch/StateForEpoch over
  * Akka remote, application.conf:11-17).  Rank 0 calls gol_comm_unique_id and
- * distributes the bytes; every rank then calls gol_comm_init. */
+ * distributes the bytes; every rank then calls gol_comm_init.  A context
+ * with a communicator always runs the ring schedule (interior rows || halo
+ * send/recv, then boundary rows); with nranks = 1 the torus ring closes on
+ * itself (send/recv to self), which runs the RCCL path on a single GPU. */
 int gol_comm_unique_id(uint8_t id_out[GOL_UNIQUE_ID_BYTES]);
 int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank, int nranks);
 

@@ -1,8 +1,20 @@
-"""GPU parity at the headline size: the 262144^2 torus of BASELINE.json
-configs[3] (8 GiB per plane), stepped one automatic 6-generation pass as one
-context (N = 1) and as an in-process group of 8 row shards of 32768 rows (the
-N = 8 decomposition and its halo schedule), bit-exact against the
-multithreaded CPU oracle: per-generation hashes and the final board."""
+"""GPU parity at the sizes and pass plans the benchmark times.
+
+* 262144^2 torus (BASELINE.json configs[3], 8 GiB per plane), 20 generations
+  -- the driver's `bench.py --steps 20`: unhashed the planner runs 6 + 6 + 8
+  (the wide G = 6 and G = 8 instances of multistep_hg_kernel, tail split
+  active at >= 32 strips), hashed 5 + 5 + 5 + 5.  As one context (N = 1), as
+  an in-process group of 8 row shards of 32768 rows (the N = 8 decomposition:
+  interior launch + boundary rows on the edge stream), and as a 1-rank RCCL
+  self-ring (the ring schedule's ncclSend / ncclRecv).
+* 65536^2 torus (configs[2]), 102 generations -- the bench's secondary run:
+  6 + 12 x 8 unhashed.
+* 262144 x 16384: the benchmark's own unhashed path on a board of 67 strips
+  with more than one round of resident waves (bulk bands + tail bands).
+
+Everything is compared with the multithreaded CPU oracle: per-generation
+hashes where the step fuses them, the final board word for word, and
+gol_hash of the final board for the unhashed path."""
 import numpy as np
 import pytest
 
@@ -11,7 +23,7 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 W = H = 262144
-GENS = 6  # one pass at the automatic depth: the benchmark's kernel
+GENS = 20  # the driver's --steps 20
 
 
 @pytest.fixture(scope="module")
@@ -20,6 +32,19 @@ def oracle_run():
     final, hashes = O.run_packed(board, W, GENS, O.TORUS, O.LIFE)
     del board
     return final, hashes
+
+
+def _unhashed_then_check(e, final, want_last):
+    e.step(GENS)  # the benchmark's own path: no fused hash
+    assert e.hash() == int(want_last)
+    assert np.array_equal(e.snapshot(), final)
+
+
+def test_full_size_262144_plans_are_the_benchs(gpu):
+    from gameoflife.engine import GolEngine
+    with GolEngine(W, H) as e:
+        assert e.pass_plan(GENS) == [6, 6, 8]
+        assert e.pass_plan(GENS, hashes=True) == [5, 5, 5, 5]
 
 
 def test_full_size_262144_one_context(gpu, oracle_run):
@@ -31,8 +56,23 @@ def test_full_size_262144_one_context(gpu, oracle_run):
         np.testing.assert_array_equal(got, want)
         assert np.array_equal(e.snapshot(), final)
         e.seed(0x5EED)
-        e.step(GENS)  # the benchmark's own path: no fused hash
-        assert e.hash() == int(want[-1])
+        _unhashed_then_check(e, final, want[-1])
+
+
+def test_full_size_262144_self_ring(gpu, oracle_run):
+    """The RCCL ring schedule on one GPU: a 1-rank communicator sends its
+    first / last G rows to itself every pass (interior || exchange, then the
+    boundary rows on the edge stream)."""
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    final, want = oracle_run
+    with GolEngine(W, H) as e:
+        e.comm_init(N.unique_id(), 0, 1)
+        e.seed(0x5EED)
+        got = e.step(GENS, hashes=True)
+        np.testing.assert_array_equal(e.allreduce_u64(got), want)
+        e.seed(0x5EED)
+        _unhashed_then_check(e, final, want[-1])
 
 
 def test_full_size_262144_eight_shards(gpu, oracle_run):
@@ -51,7 +91,52 @@ def test_full_size_262144_eight_shards(gpu, oracle_run):
         np.testing.assert_array_equal(got, want)
         for s in shards:
             assert np.array_equal(s.snapshot(), final[s.row0:s.row0 + s.rows]), s.row0
+        for s in shards:
+            s.seed(0x5EED)
+        g.step(GENS)
+        assert sum(s.hash() for s in shards) % (1 << 64) == int(want[-1])
+        for s in shards:
+            assert np.array_equal(s.snapshot(), final[s.row0:s.row0 + s.rows]), s.row0
     finally:
         g.close()
         for s in shards:
             s.close()
+
+
+def test_full_size_65536_bench_plan(gpu):
+    """configs[2]: the bench's secondary run, 102 generations (unhashed
+    6 + 12 x 8), final board and hash; hashed, every generation's hash."""
+    from gameoflife.engine import GolEngine
+    S, n = 65536, 102
+    board = O.seed_packed(S, S, 0x5EED)
+    final, want = O.run_packed(board, S, n, O.TORUS, O.LIFE)
+    del board
+    with GolEngine(S, S) as e:
+        assert sorted(e.pass_plan(n)) == [6] + [8] * 12
+        e.seed(0x5EED)
+        e.step(n)
+        assert e.hash() == int(want[-1])
+        assert np.array_equal(e.snapshot(), final)
+        e.seed(0x5EED)
+        got = e.step(n, hashes=True)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_wide_board_several_rounds_unhashed(gpu):
+    """262144 x 16384 (67 strips, > 1 round of resident waves, tail bands):
+    the unhashed planner path the headline times, against the oracle."""
+    from gameoflife.engine import GolEngine
+    Wd, Hd, n = 262144, 16384, 20
+    board = O.seed_packed(Wd, Hd, 77)
+    final, want = O.run_packed(board, Wd, n, O.TORUS, O.LIFE)
+    with GolEngine(Wd, Hd) as e:
+        assert e.pass_plan(n) == [6, 6, 8]
+        e.load(board)
+        e.step(n)
+        assert e.hash() == int(want[-1])
+        assert np.array_equal(e.snapshot(), final)
+        for gpp in (7, 8):  # every wide multi-generation depth the planner may pick
+            e.set_tuning(gens_per_pass=gpp)
+            e.load(board)
+            e.step(n)
+            assert e.hash() == int(want[-1]), gpp

@@ -324,3 +324,21 @@ def test_snapshot_into_caller_buffer(gpu):
                     np.zeros((W // 32, H), np.uint32).T):
             with pytest.raises(ValueError):
                 e.snapshot(out=bad)
+
+
+def test_step_ex_checks_hash_capacity(gpu):
+    """gol_step_ex refuses a hashes_out buffer shorter than the generations
+    asked for, before advancing anything (the JVM worker passes its direct
+    buffer's capacity)."""
+    import ctypes
+
+    from gameoflife import _native as N
+    with engine(32 * 64, 40) as e:
+        e.seed(3)
+        buf = np.zeros(4, dtype=np.uint64)
+        rc = N.lib.gol_step_ex(e._h, 5, buf.ctypes.data_as(N._u64p), buf.size)
+        assert rc == N.GOL_EINVAL and e.epoch == 0
+        assert N.lib.gol_step_ex(e._h, 4, buf.ctypes.data_as(N._u64p), buf.size) == N.GOL_OK
+        assert e.epoch == 4 and buf[-1] == e.hash()
+        assert N.lib.gol_step_ex(e._h, 3, ctypes.cast(None, N._u64p), 0) == N.GOL_OK
+        assert e.epoch == 7

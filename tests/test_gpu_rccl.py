@@ -74,3 +74,49 @@ def test_rccl_ring_matches_oracle(gpu, world, topology, gpp):
     for r in res:
         assert r[3] == [int(x) for x in want]
     assert (board == ref).all()
+
+
+# --------------------------------------------------------------------------
+# 1-rank self-ring: the RCCL ring schedule on the box's single GPU.  A context
+# with a 1-rank communicator runs gol_capi.cpp one_pass's sharded branch
+# (interior rows || ncclSend/ncclRecv of G rows to itself, then the boundary
+# rows on the edge stream after the exchange event), so every depth and the
+# rows <= 2G path are checked against the oracle here, not only in the
+# driver's multi-GPU bench.
+
+@pytest.mark.parametrize("Hs,gpp,hashed", [(97, 1, True), (203, 6, True), (203, 8, True), (203, 8, False),
+                                           (203, 0, True), (203, 0, False), (12, 8, True), (5, 8, True),
+                                           (301, 3, False)])
+def test_rccl_self_ring_matches_oracle(gpu, Hs, gpp, hashed):
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    Ws, gens = 32 * 300, 23
+    board = O.seed_packed(Ws, Hs, 1000 + Hs)
+    final, want = O.run_packed(board, Ws, gens, O.TORUS, O.LIFE)
+    with GolEngine(Ws, Hs) as e:
+        e.set_tuning(gens_per_pass=gpp)
+        e.load(board)
+        e.comm_init(N.unique_id(), 0, 1)
+        plan = e.pass_plan(gens, hashes=hashed)
+        assert max(plan) <= min(8, Hs) and sum(plan) == gens
+        got = e.step(gens, hashes=hashed)
+        if hashed:
+            np.testing.assert_array_equal(e.allreduce_u64(got), want)
+        assert e.hash() == int(want[-1])
+        assert np.array_equal(e.snapshot(), final)
+        assert e.epoch == gens
+
+
+def test_rccl_self_ring_clipped_and_rule(gpu):
+    """A clipped board has no ring neighbours (dead rows above and below):
+    the 1-rank ring schedule still runs interior + boundary launches."""
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    Wc, Hc, gens = 32 * 40 + 7, 61, 17
+    board = O.seed_packed(Wc, Hc, 3)
+    final, want = O.run_packed(board, Wc, gens, O.REF_CLIPPED, O.LIFE)
+    with GolEngine(Wc, Hc, topology="ref-clipped", rule="life") as e:
+        e.load(board)
+        e.comm_init(N.unique_id(), 0, 1)
+        np.testing.assert_array_equal(e.step(gens, hashes=True), want)
+        assert np.array_equal(e.snapshot(), final)

@@ -142,12 +142,17 @@ def test_java_random_board_matches_lcg():
         b = O.java_random_cells(6, 6, seed)
         bools = O.java_random_next_booleans(seed & ((1 << 64) - 1) if seed >= 0 else seed, 49)
         assert all(b[k % 7, k // 7] == bools[k] for k in range(49))
-    # java.util.Random(42).nextBoolean() x3 = true, false, true (well-known values
-    # of the JDK LCG: nextInt() first value for seed 42 is -1170105035)
-    s = (42 ^ 0x5DEECE66D) & ((1 << 48) - 1)
-    s = (s * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
-    v = s >> 16
-    assert v - (1 << 32) if v >= (1 << 31) else v == -1170105035
+    # External known answers of the JDK LCG: new Random(42).nextInt() is
+    # -1170105035 and new Random(0).nextInt() is -1155484576.  nextInt() =
+    # next(32) and nextBoolean() = next(1) read the same 48-bit state, so the
+    # first nextBoolean() is the sign bit of the first nextInt().
+    for seed, first_int in ((42, -1170105035), (0, -1155484576)):
+        s = (seed ^ 0x5DEECE66D) & ((1 << 48) - 1)
+        s = (s * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
+        v = s >> 16
+        signed = v - (1 << 32) if v >= (1 << 31) else v
+        assert signed == first_int, (seed, signed)
+        assert O.java_random_next_booleans(seed, 1) == [first_int < 0]
 
 
 def test_golden_ref_default_reproduces():
