@@ -597,14 +597,15 @@ int depth_cap(const gol_ctx* ctx) {
 // boxes): up to G = 6 a pass costs about the same (the sweep over the plane
 // is HBM-bound), G = 7 and 8 cost more but less per generation on wide boards
 // (>= 32 column strips); narrow boards are best at 6.
-// With the fused per-generation hash the kernels are VALU-bound from G = 5
-// on, and 5 or 6 is best everywhere (HASH=1 rows of the same sweep).
+// With the fused per-generation hash the kernels are VALU-bound from G = 6
+// on; per generation 6 is best, 7 close behind on wide boards (HASH=1 rows,
+// profiles/r02_depth_sweep_hash.txt: the one-multiply-add hash with LDS sums).
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
     // [hashed][wide]
     {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26},       // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
      {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231}},       // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
-    {{0, 0.572, 0.664, 0.682, 0.715, 0.834, 1.00, 1.248, 1.530},     // narrow, hashed
-     {0, 0.581, 0.772, 0.784, 0.771, 0.829, 1.00, 1.178, 1.410}}};   // wide, hashed
+    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.262, 1.475},     // narrow, hashed (65536^2)
+     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.186, 1.395}}};  // wide, hashed (262144^2)
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);

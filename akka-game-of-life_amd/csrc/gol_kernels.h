@@ -13,9 +13,31 @@ constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
 constexpr int kMaxGensPerPass = 8;  // temporal blocking depth supported by the kernels
 
-// Hash constants (DESIGN.md "State hash"; oracle/gol_oracle.c oracle_hash_packed).
-constexpr uint32_t kHashK1 = 0x9E3779B9u;
-constexpr uint32_t kHashK2 = 0x85EBCA6Bu;
+// State hash keys (DESIGN.md "State hash"; oracle/gol_oracle.c
+// oracle_hash_packed, oracle/oracle.py np_hash): device word w at global row
+// y, device word column c contributes w * A(y, c & 1) * B(c >> 1) mod 2^64.
+//   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * kHashRowMul (mod 2^32)
+//   A(y, 1) = A(y, 0) + kHashOddAdd        (even: stays odd)
+//   B(k)    = murmur3 fmix32(k + kHashPairAdd) | 1
+// Both keys odd, so a single-word change always changes the sum.
+constexpr uint32_t kHashRowMul = 0x9E3779B1u;
+constexpr uint32_t kHashOddAdd = 0x6A09E666u;
+constexpr uint32_t kHashPairAdd = 0x7F4A7C15u;
+
+__host__ __device__ __forceinline__ uint32_t hash_row_key(int64_t y) {
+    const uint32_t t = (uint32_t)y * kHashRowMul;
+    return ((t ^ (t >> 15)) << 1) | 1u;
+}
+
+__host__ __device__ __forceinline__ uint32_t hash_pair_key(uint32_t k) {
+    uint32_t h = k + kHashPairAdd;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h | 1u;
+}
 
 // One launch advances G generations (G = `gens`, 1..kMaxGensPerPass) over up
 // to two local row ranges, each cut into bands of its own height: the whole

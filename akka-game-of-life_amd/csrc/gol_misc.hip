@@ -89,9 +89,8 @@ __global__ void hash_kernel(const uint32_t* plane, int64_t pitch, int32_t wwords
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = k / wwords, c = k % wwords;
-        const uint32_t g = (uint32_t)((uint64_t)(grow0 + r) * (uint64_t)wwords + (uint64_t)c);
-        acc += (unsigned long long)(plane[r * pitch + c] ^ (g * kHashK1)) *
-               (unsigned long long)((g * kHashK2) | 1u);
+        const uint32_t a = hash_row_key(grow0 + r) + ((c & 1) ? kHashOddAdd : 0u);
+        acc += (unsigned long long)plane[r * pitch + c] * ((unsigned long long)a * hash_pair_key((uint32_t)(c >> 1)));
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWaveLanes);

@@ -349,28 +349,70 @@ __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (
     }
 }
 
-// Hash term accumulation for one output row (DESIGN.md "State hash").
-// lk2 holds (col + j) * K2, or -- EVENW: rows of an even number of words,
-// so the row's first global word index gb is even -- that plus the `| 1`
-// of an even product: (g K2) | 1 = g K2 + ((g & 1) ^ 1) for odd K2, and g has
-// the parity of col + j (hash_lane_k2).
-template <int VEC, bool EVENW>
-__device__ __forceinline__ void hash_row(const StepParams& p, int r, const uint32_t (&lk1)[VEC],
-                                         const uint32_t (&lk2)[VEC], const Words<VEC>& o,
-                                         unsigned long long& acc) {
-    const uint32_t gb = (uint32_t)((uint64_t)(p.grow0 + r) * (uint64_t)p.wwords);
-    const uint32_t rb1 = gb * kHashK1, rb2 = gb * kHashK2;
+// Fused state hash (DESIGN.md "State hash"): device word w at global row y,
+// device word column c contributes w * A(y, c & 1) * B(c >> 1) (mod 2^64).
+// A lane sums w * A over the rows it streams -- one v_mad_u64_u32 per word and
+// generation, the row key A an SGPR computed once per row on the scalar unit
+// -- and multiplies by its column-pair key B once, when it flushes
+// (hash_lane_total).  A lane's words share B: one pair (VEC = 2, the row's
+// first word index even), two pairs (VEC = 4: two sums), or one word of a
+// pair (VEC = 1: the lane picks the key of its word's parity).
+template <int VEC>
+struct HashAcc {
+    static constexpr int kPairs = VEC >= 2 ? VEC / 2 : 1;
+    unsigned long long a[kPairs];
+};
+
+template <int VEC>
+__device__ __forceinline__ void hash_clear(HashAcc<VEC>& h) {
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-        const uint32_t k1 = rb1 + lk1[j];
-        const uint32_t k2 = EVENW ? rb2 + lk2[j] : (rb2 + lk2[j]) | 1u;
-        acc += (unsigned long long)(o.w[j] ^ k1) * (unsigned long long)k2;
+    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k) h.a[k] = 0;
+}
+
+// One output row with row keys ae = A(y, 0), ao = A(y, 1) (both 0: the row
+// is not hashed); odd_lane: VEC = 1 lanes of odd words.
+template <int VEC>
+__device__ __forceinline__ void hash_row_keys(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
+                                              HashAcc<VEC>& h) {
+    if constexpr (VEC == 1) {
+        h.a[0] += (unsigned long long)o.w[0] * (unsigned long long)(odd_lane ? ao : ae);
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+            h.a[j / 2] += (unsigned long long)o.w[j] * (unsigned long long)((j & 1) ? ao : ae);
     }
 }
 
-template <bool EVENW>
-__device__ __forceinline__ uint32_t hash_lane_k2(int c) {
-    return (uint32_t)c * kHashK2 + (EVENW ? (((uint32_t)c & 1u) ^ 1u) : 0u);
+// One output row at global row `grow`.
+template <int VEC>
+__device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool odd_lane, HashAcc<VEC>& h) {
+    const uint32_t ae = hash_row_key(grow);
+    hash_row_keys<VEC>(ae, ae + kHashOddAdd, o, odd_lane, h);
+}
+
+// The horizontal-first kernel keeps its per-generation sums in LDS, one u64
+// per lane, pair and generation, added to with ds_add_u64 (no return): 2G
+// fewer VGPRs than register sums, which at G = 6..8 is a wave per SIMD.
+template <int VEC>
+__device__ __forceinline__ void hash_row_lds(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
+                                             unsigned long long* slot) {
+    HashAcc<VEC> t;
+    hash_clear(t);
+    hash_row_keys<VEC>(ae, ao, o, odd_lane, t);
+#pragma unroll
+    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k) atomicAdd(slot + k * kWaveLanes, t.a[k]);
+}
+
+// The lane's contribution: its sums times their column-pair keys (words
+// col .. col + VEC - 1; col even when VEC >= 2), or 0 for a lane that owns
+// no words.
+template <int VEC>
+__device__ __forceinline__ unsigned long long hash_lane_total(const HashAcc<VEC>& h, int col, bool owns) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k)
+        t += h.a[k] * (unsigned long long)hash_pair_key((uint32_t)(col >> 1) + (uint32_t)k);
+    return owns ? t : 0ull;
 }
 
 // wave reduce -> workgroup reduce -> one atomic per workgroup into a sharded slot
@@ -402,6 +444,8 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
     unsigned long long acc = 0;
 
     if (bandi < p.nbands[rg]) {
+        HashAcc<VEC> hacc;
+        hash_clear(hacc);
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
         const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
         const int nrows = r_end - r_begin;
@@ -430,12 +474,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const uint32_t rm = rvalid ? col_mask(p.vis_cols, rcol) : 0u;
             emask = lane == 0 ? lm : rm;
         }
-        uint32_t lk1[VEC], lk2[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = hash_lane_k2<PAIRS>(col + j);
-        }
+        const bool odd_lane = (col & 1) != 0;
         const bool up = (bandi & 1) != 0;
         // t-th stream row (t = 0 .. nrows+1) and i-th output row.
         auto row_of = [&](int t) -> int { return up ? r_end - t : r_begin - 1 + t; };
@@ -489,7 +528,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const int r = out_of(i);
             store_row<VEC>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
             if constexpr (HASH) {
-                if (in_band) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc);
+                if (in_band) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc);
             }
         };
 
@@ -508,7 +547,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 step_i(i, u, i < nrows);
             }
         }
-        if (!active) acc = 0;
+        if constexpr (HASH) acc = hash_lane_total(hacc, col, active);
     }
     if constexpr (HASH) hash_flush(acc, p.hash_slots, lane, wave_in_wg);
 }
@@ -548,14 +587,16 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             incol = col >= 0 && col < p.wwords;
             lcol = incol ? col : 0;
         }
-        uint32_t cmask[VEC], omask[VEC], lk1[VEC], lk2[VEC];
+        uint32_t cmask[VEC], omask[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
-            lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = hash_lane_k2<PAIRS>(col + j);
         }
+        const bool odd_lane = (col & 1) != 0;
+        HashAcc<VEC> hacc[G];
+#pragma unroll
+        for (int s = 0; s < G; ++s) hash_clear(hacc[s]);
         const bool up = (bandi & 1) != 0;
         // stream row m <-> local board row (the same for every stage)
         auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
@@ -606,7 +647,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                 if (s < G) {
                     st[s - 1][((u - s) % 3 + 3) % 3] = o;
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, PAIRS>(p, brow(m), lk1, lk2, o, acc[s - 1]);
+                        if (own_row) hash_row<VEC>(p.grow0 + brow(m), o, odd_lane, hacc[s - 1]);
                     }
                     // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
                     apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
@@ -615,7 +656,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc[G - 1]);
+                        if (own_row) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc[G - 1]);
                     }
                 }
             }
@@ -627,9 +668,9 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
 #pragma unroll
             for (int u = 0; u < kMRing; ++u) row_step(q0 + u, u);
         }
-        if (!owns) {
+        if constexpr (HASH) {
 #pragma unroll
-            for (int s = 0; s < G; ++s) acc[s] = 0;
+            for (int s = 0; s < G; ++s) acc[s] = hash_lane_total(hacc[s], col, owns);
         }
     }
     if constexpr (HASH) {
@@ -738,8 +779,19 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
     }
 }
 
+// Minimum waves per SIMD the register allocator must fit: the hashed B3/S23
+// 8-generation instance lands 4 VGPRs over the 4-wave limit (128) without it
+// (with it: 4 dwords spilled).  -DGOL_HG_MINWAVES8=1 builds the unforced
+// variant for A/B runs (scripts/ab_build.sh).
+#ifndef GOL_HG_MINWAVES8
+#define GOL_HG_MINWAVES8 4
+#endif
+template <int VEC, int G, bool LIFE, bool HASH>
+constexpr int kHgMinWaves = (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8 : 1;
+
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
-__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(const StepParams p) {
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH>)) void multistep_hg_kernel(
+    const StepParams p) {
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
     constexpr int kOut = (kWaveLanes - 2) * VEC;
@@ -750,6 +802,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
     unsigned long long acc[G];
 #pragma unroll
     for (int s = 0; s < G; ++s) acc[s] = 0;
+    __shared__ unsigned long long hash_lds[HASH ? kWavesPerWG * G * HashAcc<VEC>::kPairs * kWaveLanes : 1];
 
     if (bandi < p.nbands[rg]) {
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
@@ -770,13 +823,19 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
             incol = col >= 0 && col < p.wwords;
             lcol = incol ? col : 0;
         }
-        uint32_t cmask[VEC], omask[VEC], lk1[VEC], lk2[VEC];
+        uint32_t cmask[VEC], omask[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             cmask[j] = CLIPPED ? (incol ? col_mask(p.vis_cols, col + j) : 0u) : 0xFFFFFFFFu;
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
-            lk1[j] = (uint32_t)(col + j) * kHashK1;
-            lk2[j] = hash_lane_k2<PAIRS>(col + j);
+        }
+        const bool odd_lane = (col & 1) != 0;
+        constexpr int kNP = HashAcc<VEC>::kPairs;
+        // this lane's LDS sums: generation s, pair k at hsum[(s * kNP + k) * kWaveLanes]
+        unsigned long long* hsum = hash_lds + (size_t)wave_in_wg * G * kNP * kWaveLanes + lane;
+        if constexpr (HASH) {
+#pragma unroll
+            for (int k = 0; k < G * kNP; ++k) hsum[k * kWaveLanes] = 0ull;
         }
         const bool up = (bandi & 1) != 0;
         auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
@@ -800,6 +859,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 
         auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
 
+        // Hash row keys: stage s at stream row q hashes stream row q - s, so a
+        // shift register holds the keys of stream rows q .. q - G, 0 for rows
+        // outside the band's own rows.  Each row's keys are computed once, on
+        // the scalar unit, and no branch guards the multiply-adds.
+        uint32_t kae[G + 1], kao[G + 1];
+#pragma unroll
+        for (int k = 0; k <= G; ++k) kae[k] = kao[k] = 0u;
+
         // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF,
         // input row q arrives at ring 0, stage s produces stream row q - s.
         // Stage s has valid inputs only from q = 2s on (its rows m < s are
@@ -808,6 +875,17 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
         // kFill rows, q known at compile time -- skips those stage steps.
         auto row_step = [&](const int q, const int u, const bool fill) {
             load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
+            if constexpr (HASH) {
+#pragma unroll
+                for (int k = G; k >= 1; --k) {
+                    kae[k] = kae[k - 1];
+                    kao[k] = kao[k - 1];
+                }
+                const bool own_q = q >= G && q < n_in - G;
+                const uint32_t ae = hash_row_key(p.grow0 + brow(q));
+                kae[0] = own_q ? ae : 0u;
+                kao[0] = own_q ? ae + kHashOddAdd : 0u;
+            }
             arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
             for (int s = 1; s <= G; ++s) {
@@ -819,17 +897,12 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                                             hr[s - 1][((u - s) % 3 + 3) % 3],
                                             hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
                 const bool own_row = m >= G && m < n_in - G;
+                if constexpr (HASH) hash_row_lds<VEC>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
                 if (s < G) {
                     arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
-                    if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, PAIRS>(p, brow(m), lk1, lk2, o, acc[s - 1]);
-                    }
                 } else {
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
-                    if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, PAIRS>(p, r, lk1, lk2, o, acc[G - 1]);
-                    }
                 }
             }
         };
@@ -850,9 +923,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 #pragma unroll
             for (int u = 0; u < kMRing; ++u) row_step(q0 + u, u, false);
         }
-        if (!owns) {
+        if constexpr (HASH) {
 #pragma unroll
-            for (int s = 0; s < G; ++s) acc[s] = 0;
+            for (int s = 0; s < G; ++s) {
+                HashAcc<VEC> h;
+#pragma unroll
+                for (int k = 0; k < kNP; ++k) h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
+                acc[s] = hash_lane_total(h, col, owns);
+            }
         }
     }
     if constexpr (HASH) {

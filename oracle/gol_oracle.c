@@ -305,21 +305,40 @@ void oracle_to_pairs(uint32_t w0, uint32_t w1, uint32_t* e, uint32_t* o) {
     *o = even_bits(w0 >> 1) | (even_bits(w1 >> 1) << 16);
 }
 
-/* For every device word i = y * wwords + c of the global board (wwords = ceil(W/32)):
- *   g  = (uint32)(i mod 2^32)
- *   k1 = g * 0x9E3779B9,  k2 = (g * 0x85EBCA6B) | 1          (mod 2^32)
- *   term = (uint64)(word ^ k1) * (uint64)k2
- * hash = sum of terms mod 2^64.  A sum commutes, so the value is the same for
- * one shard or many and for any evaluation order; any single-word difference
- * always changes it (x -> (x ^ k1) * k2 is injective for odd k2).
- * Here: rows [row0, row0+rows) of a row-major board with `wwords` words per
- * row; `pairs` hashes its pair-interleaved device words instead. */
+/* Keys of the state hash (DESIGN.md "State hash"; gol_kernels.h).  Device
+ * word w at global row y and device word column c contributes
+ *   w * A(y, c & 1) * B(c >> 1)   (mod 2^64), where
+ *   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * 0x9E3779B1   (mod 2^32)
+ *   A(y, 1) = A(y, 0) + 0x6A09E666
+ *   B(k)    = fmix32(k + 0x7F4A7C15) | 1  (murmur3's 32-bit finaliser).
+ * Both keys are odd, so (A * B) is odd and any single-word difference changes
+ * the sum; a sum commutes, so the value is the same for one shard or many and
+ * for any evaluation order. */
+uint32_t oracle_hash_row_key(int64_t y, int odd) {
+    uint32_t t = (uint32_t)y * 0x9E3779B1u;
+    uint32_t a = ((t ^ (t >> 15)) << 1) | 1u;
+    return odd ? a + 0x6A09E666u : a;
+}
+
+uint32_t oracle_hash_pair_key(uint32_t k) {
+    uint32_t h = k + 0x7F4A7C15u;
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    return h | 1u;
+}
+
+/* Rows [row0, row0+rows) of a row-major board with `wwords` words per row;
+ * `pairs` hashes its pair-interleaved device words instead. */
 uint64_t oracle_hash_packed(const uint32_t* board, int64_t wwords, int64_t row0, int64_t rows,
                             int64_t pitch, int pairs) {
     uint64_t h = 0;
     /* a sum mod 2^64 commutes: rows in parallel give the same value */
 #pragma omp parallel for schedule(static) reduction(+ : h) if (rows * wwords > (1 << 20))
     for (int64_t r = 0; r < rows; ++r) {
+        const uint64_t a0 = oracle_hash_row_key(row0 + r, 0), a1 = oracle_hash_row_key(row0 + r, 1);
         for (int64_t c = 0; c < wwords; ++c) {
             uint32_t word = board[r * pitch + c];
             if (pairs) {
@@ -328,10 +347,8 @@ uint64_t oracle_hash_packed(const uint32_t* board, int64_t wwords, int64_t row0,
                 oracle_to_pairs(board[r * pitch + c0], board[r * pitch + c0 + 1], &e, &o);
                 word = (c & 1) ? o : e;
             }
-            uint32_t g = (uint32_t)((uint64_t)(row0 + r) * (uint64_t)wwords + (uint64_t)c);
-            uint32_t k1 = g * 0x9E3779B9u;
-            uint32_t k2 = (g * 0x85EBCA6Bu) | 1u;
-            h += (uint64_t)(word ^ k1) * (uint64_t)k2;
+            const uint64_t key = ((c & 1) ? a1 : a0) * (uint64_t)oracle_hash_pair_key((uint32_t)(c >> 1));
+            h += (uint64_t)word * key;
         }
     }
     return h;

@@ -70,6 +70,10 @@ def lib():
         L.oracle_hash_packed.restype = ctypes.c_uint64
         L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64, ctypes.c_int]
         L.oracle_pair_layout.argtypes = [ctypes.c_int, _i64]
+        L.oracle_hash_row_key.restype = ctypes.c_uint32
+        L.oracle_hash_row_key.argtypes = [_i64, ctypes.c_int]
+        L.oracle_hash_pair_key.restype = ctypes.c_uint32
+        L.oracle_hash_pair_key.argtypes = [ctypes.c_uint32]
         L.oracle_run_packed.argtypes = [_u32p, _u32p, _i64, _i64, _i64, ctypes.c_int,
                                         ctypes.c_uint32, ctypes.c_uint32, _i64, _i64, _i64,
                                         _u64p, ctypes.c_int]
@@ -199,16 +203,28 @@ def np_device_words(packed: np.ndarray, W: int, topology: int = TORUS) -> np.nda
 
 
 def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
-    """Same hash spec as gol_oracle.c, written independently with numpy."""
+    """Same hash spec as gol_oracle.c (DESIGN.md "State hash"), written
+    independently with numpy: sum of w * A(y, c & 1) * B(c >> 1) mod 2^64."""
     ww = wwords(W)
     p = np_device_words(packed, W, topology).astype(np.uint64)
     rows = p.shape[0]
-    g = ((np.arange(rows, dtype=np.uint64)[:, None] + np.uint64(row0)) * np.uint64(ww)
-         + np.arange(ww, dtype=np.uint64)[None, :]) & np.uint64(0xFFFFFFFF)
-    k1 = (g * np.uint64(0x9E3779B9)) & np.uint64(0xFFFFFFFF)
-    k2 = ((g * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)) | np.uint64(1)
+    m32 = np.uint64(0xFFFFFFFF)
     with np.errstate(over="ignore"):
-        terms = (p ^ k1) * k2
+        y = np.arange(rows, dtype=np.uint64) + np.uint64(row0)
+        t = (y * np.uint64(0x9E3779B1)) & m32
+        a0 = ((((t ^ (t >> np.uint64(15))) << np.uint64(1)) | np.uint64(1)) & m32)
+        a1 = (a0 + np.uint64(0x6A09E666)) & m32
+        k = np.arange(ww, dtype=np.uint64) >> np.uint64(1)
+        h = (k + np.uint64(0x7F4A7C15)) & m32
+        h ^= h >> np.uint64(16)
+        h = (h * np.uint64(0x85EBCA6B)) & m32
+        h ^= h >> np.uint64(13)
+        h = (h * np.uint64(0xC2B2AE35)) & m32
+        h ^= h >> np.uint64(16)
+        b = h | np.uint64(1)
+        odd = (np.arange(ww) & 1).astype(bool)
+        a = np.where(odd[None, :], a1[:, None], a0[:, None])
+        terms = p * (a * b[None, :])
         return int(terms.sum(dtype=np.uint64))
 
 

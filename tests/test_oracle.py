@@ -129,6 +129,31 @@ def test_hash_properties():
         assert O.hash_packed(b2, 320) != h
 
 
+def test_hash_keys_odd_and_structured_moves_detected():
+    """The keys are odd (a single-word change always changes the hash), and
+    the moves Life makes -- a pattern translated by one row or column, or
+    two cells of a column moving apart symmetrically (the move a row key
+    linear in y could not see) -- change it."""
+    for y in (0, 1, 2, 1000, 262143, (1 << 30) - 1):
+        assert O.lib().oracle_hash_row_key(y, 0) & 1 and O.lib().oracle_hash_row_key(y, 1) & 1
+    for k in (0, 1, 4095, 1 << 20):
+        assert O.lib().oracle_hash_pair_key(k) & 1
+    W, H = 256, 64
+    glider = np.zeros((H, W), dtype=np.uint8)
+    for x, y in [(11, 10), (12, 11), (10, 12), (11, 12), (12, 12)]:
+        glider[y, x] = 1
+    seen = set()
+    for dy in range(0, 40):
+        for dx in range(0, 70):
+            seen.add(O.hash_packed(O.pack(np.roll(np.roll(glider, dy, 0), dx, 1)), W))
+    assert len(seen) == 40 * 70
+    base = np.zeros((H, W), dtype=np.uint8)
+    for d in range(1, 12):
+        a = base.copy(); a[30 - d, 77] = a[30 + d, 77] = 1
+        b = base.copy(); b[30 - d - 1, 77] = b[30 + d + 1, 77] = 1
+        assert O.hash_packed(O.pack(a), W) != O.hash_packed(O.pack(b), W)
+
+
 def test_seed_sharding_invariant():
     full = O.seed_packed(1000, 50, 9)
     assert (full == O.np_seed(1000, 50, 9)).all()
