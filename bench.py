@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""bench.py -- generation-step throughput (GCUPS) + HBM roofline fraction.
+"""bench.py -- generation-step throughput (GCUPS) and its roofline.
 
 Workload (BASELINE.json configs[3], DESIGN.md "Measurement"): a 262144 x
 262144 torus, B3/S23, Bernoulli(0.5) splitmix64 board (seed 0x5EED),
@@ -12,9 +12,19 @@ under "secondary".
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 value = W*H*K / max-over-ranks wall time of the K timed generations (GCUPS),
-with the board already resident in HBM.  roofline.achieved = algorithmic bytes
-(0.25 B per cell-update: 1 bit read + 1 bit written) per step-kernel launch /
-the launch's average duration from HIP events on the launch stream.
+with the board already resident in HBM.
+
+roofline: the dominant kernel (the whole-shard launch at
+N = 1, a shard's interior-rows launch at N > 1) is bound by VALU issue, not by
+HBM -- temporal blocking fuses 6-8 generations per pass over the plane.  So:
+  * roofline.bound = "valu": achieved = cell-updates per second of that launch
+    (cells x generations per launch / its mean HIP-event duration), peak = the
+    VALU-issue ceiling of the kernel's loop mix at the clock the chip held
+    during those launches (PMC GRBM_GUI_ACTIVE, profiles/pmc_launch.json);
+  * roofline.traffic = PMC HBM bytes per launch, and roofline.hbm the physical
+    HBM bandwidth that implies against the 8 TB/s spec;
+  * roofline.hbm_effective = SURVEY.md section 8(d)'s 2 bits per cell-update,
+    counted per generation: above 1 by construction of temporal blocking.
 """
 from __future__ import annotations
 
@@ -29,7 +39,19 @@ sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_CELL_UPDATE = 0.25
+CLOCK_MAX_GHZ = 2.4  # MI355X_MICROARCH.md max clock
+SIMDS = 256 * 4
+CELLS_PER_WAVE_INSTR = 64 * 32  # 64 lanes x one 32-cell word
 DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass_plan, DESIGN.md "Pass planner")
+
+# Issue-cost model of the multi-generation kernel's loop (DESIGN.md "Roofline"):
+# VALU instructions per 32-cell word and generation of multistep_hg_kernel<2, G,
+# LIFE> on the pair layout (scripts/isa_loop.py census: at G = 6, 800 VALU per
+# 6-row unroll = 648 bitop3 + 72 alignbit + 72 DPP + loop overhead) and the
+# measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
+VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
+# The fused hash adds one v_mad_u64_u32 per word and generation (DESIGN.md "State hash").
+VALU_MIX_HASH = dict(VALU_MIX, v_mad_u64_u32=(1, 4.6))
 
 
 def parse():
@@ -44,6 +66,7 @@ def parse():
                     help="generations fused per HBM pass (temporal blocking depth 1..8; 0 = automatic)")
     ap.add_argument("--hash", action="store_true", help="fuse the per-generation state hash")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-ring", action="store_true", help="skip the N = 1 ring-schedule measurements")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     return ap.parse_args()
@@ -90,12 +113,27 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
     return dt, kms, launches, gens
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(width, seconds):
     """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
-    workload: a torus of the same width and 1024 rows, run for ~`seconds`."""
+    workload: a torus of the same width and 1024 rows, run for ~`seconds`, on
+    every core this process may use -- the CPU share the harness grants the
+    job (OMP_NUM_THREADS, 16 threads per GPU on the pool's boxes), else every
+    core of sched_getaffinity."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or threads)
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(share, affinity) if share > 0 else affinity
     H = 1024
     board = O.seed_packed(width, H, 0x5EED)
     O.run_packed(board, width, 1, nthreads=threads, want_hashes=False)  # warm
@@ -105,24 +143,92 @@ def cpu_baseline(width, seconds):
         gens += 4
     dt = time.perf_counter() - t0
     return {"value": round(width * H * gens / dt / 1e9, 3), "unit": "GCUPS", "cores": threads,
-            "kind": "port",
-            "sample": f"oracle_run_packed (oracle/gol_oracle.c), {width}x{H} torus B3/S23 slice of "
-                      f"the same workload, {gens} generations in {dt:.1f} s, {threads} OpenMP threads"}
+            "kind": "port", "nproc": affinity, "cpu_model": cpu_model(),
+            "threads_source": "OMP_NUM_THREADS (the job's CPU share)" if share > 0 else "sched_getaffinity",
+            "sample": f"oracle_run_packed (oracle/gol_oracle.c, bit-sliced, OpenMP), {width}x{H} torus B3/S23 "
+                      f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
 
 
-def roofline(kms, launches, gens_covered, cells_per_gen_per_launch):
-    """Algorithmic bytes per launch (0.25 B per cell-update x cells x the
-    generations one launch advances) / the launch's average duration."""
+def pmc_launch():
+    """profiles/pmc_launch.json (scripts/gpu_pmc.sh + scripts/pmc_launch.py):
+    per-launch PMC numbers keyed 'WxH/mode/G<g>/h<hash>'."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_launch.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def plan_pmc(shape, mode, plan, hashed):
+    """PMC numbers of a pass plan's launches: mean HBM bytes per launch,
+    time-weighted clock, cell-weighted VALU per word-generation.  None if a
+    depth of the plan was not profiled."""
+    table = pmc_launch()
+    ents = [table.get(f"{shape}/{mode}/G{g}/h{int(hashed)}") for g in plan]
+    if not ents or any(e is None for e in ents):
+        return None
+    t = sum(e["launch_ms"] for e in ents)
+    return {"hbm_bytes": sum(e["hbm_bytes"] for e in ents) / len(ents),
+            "clock_ghz": sum(e["clock_ghz"] * e["launch_ms"] for e in ents) / t,
+            "valu_per_word_gen": sum(e["valu_per_word_gen"] * e["generations_per_launch"] for e in ents) /
+            sum(e["generations_per_launch"] for e in ents),
+            "keys": sorted({f"{shape}/{mode}/G{g}/h{int(hashed)}" for g in plan})}
+
+
+def valu_peak_gcups(mix, clock_ghz):
+    cycles = sum(n * c for n, c in mix.values())
+    return SIMDS * clock_ghz * 1e9 / cycles * CELLS_PER_WAVE_INSTR / 1e9, cycles
+
+
+def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False):
+    """Roofline of the dominant kernel (see the module docstring)."""
     if not launches:
         return None
     avg_s = kms / 1e3 / launches
     gpl = gens_covered / launches
-    algo = cells_per_gen_per_launch * gpl * BYTES_PER_CELL_UPDATE
-    ach = algo / avg_s / 1e9
-    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-            "avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches,
-            "generations_per_launch": gpl, "algorithmic_bytes_per_launch": algo}
+    gcups = cells * gpl / avg_s / 1e9
+    algo = cells * gpl * BYTES_PER_CELL_UPDATE
+    common = {"avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches, "generations_per_launch": gpl,
+              "pass_plan": plan}
+    pmc = plan_pmc(shape, mode, plan, hashed)
+    if set(plan) == {1}:  # single-generation passes: a stream over the plane, HBM-bound
+        r = {"bound": "hbm", "achieved": round(algo / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(algo / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+             "algorithmic_bytes_per_launch": algo, **common}
+        if pmc:
+            r["traffic"] = round(pmc["hbm_bytes"])
+            r["measured_hbm_gbs"] = round(pmc["hbm_bytes"] / avg_s / 1e9, 1)
+            r["measured_hbm_frac"] = round(pmc["hbm_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS, 4)
+            r["traffic_source"] = "profiles/pmc_launch.json " + ", ".join(pmc["keys"])
+        return r
+    mix = VALU_MIX_HASH if hashed else VALU_MIX
+    clock = pmc["clock_ghz"] if pmc else CLOCK_MAX_GHZ
+    peak, cycles = valu_peak_gcups(mix, clock)
+    peak_max, _ = valu_peak_gcups(mix, CLOCK_MAX_GHZ)
+    r = {"bound": "valu", "achieved": round(gcups, 1), "peak": round(peak, 1), "unit": "GCUPS",
+         "frac": round(gcups / peak, 4), "traffic": round(pmc["hbm_bytes"]) if pmc else None,
+         "clock_ghz": round(clock, 3),
+         "clock_source": ("PMC GRBM_GUI_ACTIVE / 8 / launch time, time-weighted over the plan "
+                          "(profiles/pmc_launch.json)") if pmc else "max clock (no PMC entry for this plan)",
+         "frac_at_max_clock": round(gcups / peak_max, 4),
+         "valu": {"instructions_per_word_generation": {k: n for k, (n, _) in mix.items()},
+                  "cycles_per_word_generation": round(cycles, 2),
+                  "peak_gcups_at_max_clock": round(peak_max, 1),
+                  "measured_valu_per_word_generation": round(pmc["valu_per_word_gen"], 2) if pmc else None,
+                  "source": "loop census scripts/isa_loop.py; issue costs profiles/r01_valu_op_costs.txt"},
+         **common}
+    if pmc:
+        gbs = pmc["hbm_bytes"] / avg_s / 1e9
+        r["hbm"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4),
+                    "note": "physical HBM traffic per launch (PMC FETCH_SIZE x2 + WRITE_SIZE) / launch time",
+                    "traffic_source": "profiles/pmc_launch.json " + ", ".join(pmc["keys"])}
+    r["hbm_effective"] = {"achieved": round(algo / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(algo / avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                          "algorithmic_bytes_per_launch": algo,
+                          "note": "0.25 B per cell-update (SURVEY.md 8d) x generations fused per launch: "
+                                  "exceeds 1 by temporal blocking, not a bandwidth"}
+    return r
 
 
 def kernel_label(info, depths):
@@ -141,48 +247,6 @@ def kernel_label(info, depths):
     return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE> ({waves} waves/CU resident)"
 
 
-def traffic_key(W, H, world, gpp, steps):
-    """profiles/pmc_traffic.json key: fixed depth G, or the automatic plan of
-    `steps` generations (scripts/prof_run.py runs the same plan)."""
-    return f"{W}x{H}/N{world}/G{gpp}" if gpp else f"{W}x{H}/N{world}/auto{steps}"
-
-
-# Issue-cost model of the multi-generation kernel (DESIGN.md "Roofline"):
-# VALU instructions per 32-cell word and generation in the loop of
-# multistep_hg_kernel<2, G, LIFE> on the pair layout (from its ISA), and the
-# measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
-# per 32-cell word and generation in the hg kernel's loop (full-sum rule circuit,
-# scripts/isa_loop.py census: 800 VALU per 6-row unroll at G = 6 = 72 DPP + 72
-# alignbit + 648 bitop3 + loop overhead), issue costs from op_cost.hip
-VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
-SIMDS = 256 * 4
-CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md max clock
-
-
-def valu_roofline(gcups):
-    """Cell-update rate the VALU issue model allows at the max clock (every
-    SIMD issuing the loop's instruction mix back to back), and the fraction
-    of it the run reached.  Halo lanes and band halo rows are overheads
-    counted against the kernel, not removed from the peak."""
-    cycles = sum(n * c for n, c in VALU_MIX.values())
-    peak = SIMDS * CLOCK_GHZ * 1e9 / cycles * 64 * 32 / 1e9
-    return {"bound": "valu", "instructions_per_word_generation": {k: n for k, (n, _) in VALU_MIX.items()},
-            "cycles_per_word_generation": round(cycles, 2), "clock_ghz": CLOCK_GHZ,
-            "peak_gcups": round(peak, 1), "frac": round(gcups / peak, 4),
-            "source": "profiles/r01_valu_op_costs.txt (scripts/micro/op_cost.hip)"}
-
-
-def pmc_traffic(workload_key):
-    """HBM bytes per launch measured with rocprofv3 --pmc (profiles/pmc_traffic.json,
-    written by scripts/pmc_traffic.py with the gfx950 FETCH_SIZE x2 correction)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            return json.load(f).get(workload_key)
-    except (OSError, ValueError):
-        return None
-
-
 def secondary_run(GolEngine, torch, dist, a, local):
     """BASELINE.json configs[2]: the 65536^2 single-GPU roofline run."""
     S = 65536
@@ -190,16 +254,18 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
         e2.seed(0x5EED)
         # >= 10 warm-up and >= 100 timed
-        # generations, rounded up to whole 6-generation passes
+        # generations, rounded up to whole passes
         n2, w2 = max(a.steps, 102), max(a.warmup, 12)
         dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
+        plan2 = e2.pass_plan(n2, hashes=a.hash)
         # the same board one generation per HBM pass: the pure bandwidth case
         # (north_star: >= 70 % of peak HBM bandwidth at 65536^2)
         e2.set_tuning(band_rows=a.band, gens_per_pass=1)
         e2.seed(0x5EED)
         dt1, kms1, l1, g1 = timed_run(e2, torch, dist, 1, n2, w2, a.hash)
-    r2 = with_traffic(roofline(kms2, l2, g2, S * S), traffic_key(S, S, 1, a.gpp, n2))
-    r1 = with_traffic(roofline(kms1, l1, g1, S * S), f"{S}x{S}/N1/G1")
+    shape = f"{S}x{S}"
+    r2 = roofline(kms2, l2, g2, S * S, plan2, shape, "N1", a.hash)
+    r1 = roofline(kms1, l1, g1, S * S, [1] * n2, shape, "N1", a.hash)
     return {"workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])",
             "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": w2,
             "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2,
@@ -207,20 +273,32 @@ def secondary_run(GolEngine, torch, dist, a, local):
                                          "ms_per_step": round(dt1 / n2 * 1e3, 4), "roofline": r1}}
 
 
-def with_traffic(r, key):
-    """Add the PMC-measured HBM bytes per launch (and the bandwidth they
-    imply at the measured launch time) to a roofline object."""
-    if r is None:
-        return None
-    t = pmc_traffic(key)
-    if t is not None:
-        r["traffic"] = t.get("hbm_bytes_per_launch")
-        r["traffic_source"] = t.get("source")
-        if r["traffic"]:
-            gbs = r["traffic"] / (r["avg_launch_ms"] * 1e-3) / 1e9
-            r["measured_hbm_gbs"] = round(gbs, 1)
-            r["measured_hbm_frac"] = round(gbs / HBM_PEAK_GBS, 4)
-    return r
+def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
+    """N = 1 only: the row-sharded (RCCL ring) schedule on this GPU, as a 1-rank
+    self-ring (gol_capi.cpp one_pass: interior launch || G-row halo
+    ncclSend/ncclRecv to itself, then the boundary rows on the edge stream).
+    (1) the whole board, (2) one rank's shard of the N = 8 decomposition
+    (262144 x 32768): what each of 8 ranks computes, without the xGMI latency
+    of a real ring."""
+    out = {}
+    eng.comm_init(N.unique_id(), 0, 1)
+    eng.seed(0x5EED)
+    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
+    out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
+                                    "ms_per_step": round(dt / a.steps * 1e3, 4),
+                                    "pass_plan": eng.pass_plan(min(a.steps, 1024))}
+    rows8 = H // 8
+    with GolEngine(W, H, topology="torus", rule="life", device=local, row0=0, rows=rows8) as e8:
+        e8.comm_init(N.unique_id(), 0, 1)  # a 1-rank ring over a shard-sized torus
+        e8.seed(0x5EED)
+        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        plan8 = e8.pass_plan(min(a.steps, 1024))
+    out["per_rank_shard_self_ring"] = {
+        "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
+        "unit": "GCUPS", "ms_per_step": round(dt8 / a.steps * 1e3, 4), "pass_plan": plan8,
+        "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
+                                    f"{W}x{rows8}", "ring")}
+    return out
 
 
 def main():
@@ -252,25 +330,26 @@ def main():
     hashed = None
     if world == 1 and not a.hash:
         # the same workload with the fused per-generation state hash (the
-        # parity contract's output: one u64 per generation, DESIGN.md §5),
+        # parity contract's output: one u64 per generation, DESIGN.md section 5),
         # continuing from the board the timed run left
-        dth, _, _, _ = timed_run(eng, torch, dist, world, a.steps, 1, True)
-        hashed = {"value": round(W * H * a.steps / dth / 1e9, 2), "unit": "GCUPS",
-                  "ms_per_step": round(dth / a.steps * 1e3, 4),
-                  "pass_plan": eng.pass_plan(min(a.steps, 1024), hashes=True)}
+        dth, kmsh, lh, gh = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
+        hplan = eng.pass_plan(min(a.steps, 1024), hashes=True)
+        vh = W * H * a.steps / dth / 1e9
+        hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
+                  "frac_of_unhashed": round(vh / value, 4), "pass_plan": hplan,
+                  "roofline": roofline(kmsh, lh, gh, W * H, hplan, f"{W}x{H}", "N1", True)}
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
     G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
-    cells = W * (rows if world == 1 else max(rows - round(2 * G), 0))
-    roof = roofline(kms, launches, gcov, cells)
-    key = traffic_key(W, H, world, a.gpp, a.steps)
+    if world == 1:
+        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash)
+    else:
+        roof = roofline(kms, launches, gcov, W * max(rows - round(2 * G), 0), plan, f"{W}x{rows}", "ring", a.hash)
     if roof is not None:
         roof["kernel"] = kernel_label(eng_info, plan)
-        roof["pass_plan"] = plan
-        if "multistep_hg_kernel<2," in roof["kernel"] and N.pair_layout(W):
-            # per-launch rate of the dominant kernel, not the wall-clock value
-            roof["valu"] = valu_roofline(cells * gcov / launches / (roof["avg_launch_ms"] * 1e-3) / 1e9)
-        with_traffic(roof, key)
+    ring = None
+    if world == 1 and not a.no_ring and not a.hash:
+        ring = ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H)
     out = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 2),
@@ -287,13 +366,16 @@ def main():
         "config": {"workload": f"{W}x{H} torus B3/S23 row-sharded over {world} GPU(s) "
                                f"(BASELINE.json configs[3]; N=1 = whole board on one GPU)",
                    "board": [W, H], "rule": "B3/S23", "topology": "torus",
-                   "parallelism": f"row-block x{world}, RCCL halo send/recv",
+                   "parallelism": ("single GPU, whole board (no halo exchange)" if world == 1 else
+                                   f"row-block x{world}, G-deep RCCL halo send/recv per pass (ring over xGMI)"),
                    "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash)},
         "roofline": roof,
     }
     if hashed is not None:
         out["with_state_hash"] = hashed
+    if ring is not None:
+        out["ring_schedule_n1"] = ring
     eng.close()
 
     if rank == 0 and world == 1:

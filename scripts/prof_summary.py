@@ -5,12 +5,9 @@
 * <tag>_kernel_trace.txt      per-(kernel, grid) dispatch durations of the same
                               command, beside the bench's own HIP-event numbers
 * <tag>_bench.json            the bench line printed under rocprofv3 and unprofiled
-* pmc_traffic.json            HBM bytes per step launch from separate --pmc passes
 
-HBM bytes (MI355X_MICROARCH.md "HBM"): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reads exactly half the bytes of a 16-B-per-lane
-streaming read, so hbm = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  The G=1
-kernel's WRITE_SIZE equals one plane exactly, which checks the unit.
+Per-launch PMC numbers (HBM bytes, clock, VALU issue) come from
+scripts/gpu_pmc.sh + scripts/pmc_launch.py (profiles/pmc_launch.json).
 
     python3 scripts/prof_summary.py [prof_dir] [tag]
 """
@@ -76,46 +73,12 @@ def main():
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
-    traffic = {}
-    for edge in (262144, 65536):
-        for g in (0, 1):
-            fdir = os.path.join(prof, f"pmc_FETCH_SIZE_{edge}_g{g}", "run_counter_collection.csv")
-            wdir = os.path.join(prof, f"pmc_WRITE_SIZE_{edge}_g{g}", "run_counter_collection.csv")
-            if not (os.path.exists(fdir) and os.path.exists(wdir)):
-                continue
-            fetch = pmc_per_dispatch(fdir, "FETCH_SIZE")
-            write = pmc_per_dispatch(wdir, "WRITE_SIZE")
-            # g = 0: the automatic pass plan of the bench's generation count
-            # (mixed depths: per-launch means), g = 1: single-generation passes
-            gens = GENS[edge] if g == 0 else 60
-            n = min(len(fetch), len(write))
-            fetch, write = fetch[:n], write[:n]
-            G = gens / n if g == 0 else 1  # generations per launch
-            f_b, w_b = 2 * statistics.fmean(fetch) * 1024, statistics.fmean(write) * 1024
-            hbm = f_b + w_b
-            plane = edge * edge / 8
-            key = f"{edge}x{edge}/N1/auto{gens}" if g == 0 else f"{edge}x{edge}/N1/G1"
-            traffic[key] = {
-                "hbm_bytes_per_launch": round(hbm),
-                "fetch_bytes_per_launch": round(f_b),
-                "write_bytes_per_launch": round(w_b),
-                "planes_read": round(f_b / plane, 3),
-                "planes_written": round(w_b / plane, 3),
-                "generations_per_launch": round(G, 3),
-                "algorithmic_bytes_per_launch": edge * edge * 0.25 * G,
-                "hbm_bytes_per_cell_generation": round(hbm / (edge * edge * G), 4),
-                "launches_measured": n,
-                "source": f"profiles/{tag}_pmc (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-                          f"scripts/prof_run.py {edge} {gens} {g}; FETCH_SIZE x2 gfx950 correction)"}
-    with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
     pdir = os.path.join(dst, f"{tag}_pmc")
     os.makedirs(pdir, exist_ok=True)
     for d in sorted(os.listdir(prof)):
         src = os.path.join(prof, d, "run_counter_collection.csv")
         if d.startswith("pmc_") and os.path.exists(src):
             shutil.copy(src, os.path.join(pdir, f"{d}.csv"))
-    print(json.dumps(traffic, indent=1))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,51 @@
+"""bench.py's roofline fields (CPU: pure functions over a synthetic PMC
+table).  The dominant multi-generation kernel is reported against the VALU
+issue ceiling at the PMC-measured clock (frac <= 1 for any rate the model
+allows), with the physical HBM fraction and the 2-bit/cell/generation
+'effective' figure beside it; single-generation passes stay HBM-bound."""
+import bench
+
+
+def _table(monkeypatch, entries):
+    monkeypatch.setattr(bench, "pmc_launch", lambda: entries)
+
+
+def test_valu_roofline_with_pmc(monkeypatch):
+    ent = lambda g, ms, clk: {"launch_ms": ms, "hbm_bytes": 18e9, "clock_ghz": clk, "valu_per_word_gen": 12.0,
+                              "generations_per_launch": g}
+    _table(monkeypatch, {"262144x262144/N1/G6/h0": ent(6, 4.0, 2.0), "262144x262144/N1/G8/h0": ent(8, 5.0, 1.9)})
+    cells = 262144 * 262144
+    r = bench.roofline(kms=13.0, launches=3, gens_covered=20, cells=cells, plan=[6, 6, 8],
+                       shape="262144x262144", mode="N1")
+    assert r["bound"] == "valu" and r["unit"] == "GCUPS"
+    clock = (2.0 * 4 + 2.0 * 4 + 1.9 * 5) / 13
+    assert abs(r["clock_ghz"] - round(clock, 3)) < 1e-3
+    peak = 1024 * clock * 2048 / 29.1
+    achieved = cells * 20 / 3 / (13.0 / 3 / 1e3) / 1e9
+    assert abs(r["peak"] - peak) < 1.0 and abs(r["achieved"] - achieved) < 1.0
+    assert abs(r["frac"] - achieved / peak) < 1e-3 and r["frac"] < 1
+    assert r["traffic"] == 18e9
+    assert r["hbm"]["frac"] < 1 and r["hbm_effective"]["frac"] > 1
+
+
+def test_missing_pmc_entry_falls_back_to_max_clock(monkeypatch):
+    _table(monkeypatch, {})
+    r = bench.roofline(kms=10.0, launches=2, gens_covered=16, cells=1 << 30, plan=[8, 8],
+                       shape="65536x16384", mode="ring")
+    assert r["traffic"] is None and r["clock_ghz"] == bench.CLOCK_MAX_GHZ
+    assert r["frac"] == r["frac_at_max_clock"] and "hbm" not in r
+
+
+def test_single_generation_passes_are_hbm_bound(monkeypatch):
+    _table(monkeypatch, {"65536x65536/N1/G1/h0": {"launch_ms": 0.2, "hbm_bytes": 1.1e9, "clock_ghz": 2.1,
+                                                  "valu_per_word_gen": 20.0, "generations_per_launch": 1}})
+    r = bench.roofline(kms=20.4, launches=102, gens_covered=102, cells=65536 * 65536, plan=[1] * 102,
+                       shape="65536x65536", mode="N1")
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0.5 < r["frac"] < 1
+    assert r["traffic"] == 1100000000 and r["measured_hbm_frac"] < 1
+
+
+def test_hashed_mix_adds_the_multiply_add():
+    p0, c0 = bench.valu_peak_gcups(bench.VALU_MIX, 2.4)
+    p1, c1 = bench.valu_peak_gcups(bench.VALU_MIX_HASH, 2.4)
+    assert abs(c1 - c0 - 4.6) < 1e-9 and p1 < p0
