@@ -349,13 +349,21 @@ int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bo
     return waves;
 }
 
+// Rows of the plane a launch steps and the global row of its local row 0:
+// the context's own (default), or gol_replay's extended block.
+struct PlaneGeom {
+    int32_t rows;
+    int64_t grow0;
+};
+
 // Launch one pass of `gens` generations over local row ranges [lo0,hi0)
 // (+ [lo1,hi1) if n == 2).  Only the main launch of a pass (whole shard, or
 // the interior rows of a sharded shard) is bracketed by profiling events: it
 // is the dominant kernel.
 int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
                   const uint32_t* hbot, int64_t halo_stride, bool wrap_y, unsigned long long* slots, int n,
-                  const int32_t* lo, const int32_t* hi, bool main_launch, hipStream_t stream = nullptr) {
+                  const int32_t* lo, const int32_t* hi, bool main_launch, hipStream_t stream = nullptr,
+                  const PlaneGeom* geom = nullptr) {
     if (!stream) stream = ctx->compute;
     gol::StepParams p{};
     p.cur = cur;
@@ -366,12 +374,12 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wrap_y = wrap_y ? 1 : 0;
     p.hash_slots = slots;
     p.pitch = ctx->pitch;
-    p.grow0 = ctx->row0;
+    p.grow0 = geom ? geom->grow0 : ctx->row0;
     p.vis_rows = ctx->topology == GOL_TORUS ? ctx->height : ctx->vis_h;
     p.vis_cols = ctx->topology == GOL_TORUS ? ctx->width : ctx->vis_w;
     p.width = ctx->width;
     p.wwords = ctx->wwords;
-    p.rows = (int32_t)ctx->rows;
+    p.rows = geom ? geom->rows : (int32_t)ctx->rows;
     const int vec = lane_words(ctx, gens);
     const int sw = gol::strip_words(vec, gens);
     p.strips = (int32_t)((ctx->wwords + sw - 1) / sw);
@@ -901,6 +909,107 @@ int gol_step_ex(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out, size_t
         return set_err(ctx, GOL_EINVAL, "hashes_out holds %zu entries, %u generations requested", hashes_capacity,
                        generations);
     return gol_step(ctx, generations, hashes_out);
+}
+
+int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const uint32_t* below,
+               int64_t host_pitch_words, uint64_t* hashes_out) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (generations == 0) return GOL_OK;
+    if (!above || !below) return set_err(ctx, GOL_EINVAL, "null light-cone rows");
+    if (host_pitch_words < ctx->wwords)
+        return set_err(ctx, GOL_EINVAL, "host pitch %lld < words per row %d", (long long)host_pitch_words,
+                       ctx->wwords);
+    if (ctx->group || ctx->nccl)
+        return set_err(ctx, GOL_ESTATE, "replay a shard before it joins its group or ring");
+    const int64_t n = generations;
+    const int64_t ext = ctx->rows + 2 * n;
+    if (ext > (1 << 30)) return set_err(ctx, GOL_EINVAL, "light cone too deep");
+    if (int rc = bind(ctx)) return rc;
+    if (hashes_out) {
+        if (int rc = ensure_slots(ctx, generations)) return rc;
+        HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, (size_t)n * gol::kHashGenStride * sizeof(unsigned long long),
+                                      ctx->compute));
+    }
+    const size_t bytes = (size_t)ext * ctx->pitch * sizeof(uint32_t);
+    uint32_t* blk[2] = {nullptr, nullptr};
+    auto release = [&]() {
+        hipStreamSynchronize(ctx->compute);
+        for (auto* b : blk)
+            if (b) hipFree(b);
+    };
+    for (auto*& b : blk) {
+        if (hipMalloc(&b, bytes) != hipSuccess) {
+            release();
+            return set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes for the light cone failed", bytes);
+        }
+    }
+    // The extended block: n rows above, the shard's rows, n rows below, as
+    // they were at the shard's epoch.  Host rows are row-major; a pair-layout
+    // board converts them on the device (upload to the other block first).
+    const int64_t pitch = ctx->pitch, hp = host_pitch_words;
+    uint32_t* up = ctx->pairs ? blk[1] : blk[0];
+    auto fail_hip = [&](hipError_t e, const char* what) {
+        release();
+        return set_err(ctx, GOL_EHIP, "%s failed: %s", what, hipGetErrorString(e));
+    };
+    hipError_t e = hipMemsetAsync(blk[0], 0, bytes, ctx->compute);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(up, pitch * 4, above, hp * 4, (size_t)ctx->wwords * 4, n, hipMemcpyHostToDevice,
+                             ctx->compute);
+    if (e == hipSuccess)
+        e = hipMemcpy2DAsync(up + (n + ctx->rows) * pitch, pitch * 4, below, hp * 4, (size_t)ctx->wwords * 4, n,
+                             hipMemcpyHostToDevice, ctx->compute);
+    if (e == hipSuccess && ctx->pairs) {
+        e = gol::launch_convert(up, blk[0], pitch, ctx->wwords, (int32_t)n, true, ctx->compute);
+        if (e == hipSuccess)
+            e = gol::launch_convert(up + (n + ctx->rows) * pitch, blk[0] + (n + ctx->rows) * pitch, pitch,
+                                    ctx->wwords, (int32_t)n, true, ctx->compute);
+    }
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(blk[0] + n * pitch, ctx->plane[ctx->cur], (size_t)ctx->rows * pitch * 4,
+                           hipMemcpyDeviceToDevice, ctx->compute);
+    if (e != hipSuccess) return fail_hip(e, "light-cone upload");
+    // One generation per pass over the whole block; rows beyond it read as
+    // dead (their garbage moves one row per generation and never reaches the
+    // shard's rows).  Each generation's partial hash covers the shard's rows.
+    const PlaneGeom geom{(int32_t)ext, ctx->row0 - n};
+    const int32_t lo[1] = {0}, hi[1] = {(int32_t)ext};
+    int cur = 0;
+    for (int64_t g = 0; g < n; ++g) {
+        if (int rc = launch_ranges(ctx, 1, blk[cur], blk[cur ^ 1], ctx->zero_row, ctx->zero_row, 0, false, nullptr, 1,
+                                   lo, hi, false, ctx->compute, &geom)) {
+            release();
+            return rc;
+        }
+        cur ^= 1;
+        if (hashes_out) {
+            e = gol::launch_hash(blk[cur] + n * pitch, pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
+                                 ctx->slots + (size_t)g * gol::kHashGenStride, ctx->compute);
+            if (e != hipSuccess) return fail_hip(e, "light-cone hash");
+        }
+    }
+    e = hipMemcpyAsync(ctx->plane[ctx->cur], blk[cur] + n * pitch, (size_t)ctx->rows * pitch * 4,
+                       hipMemcpyDeviceToDevice, ctx->compute);
+    if (e == hipSuccess && hashes_out)
+        e = hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, (size_t)n * gol::kHashGenStride * 8,
+                           hipMemcpyDeviceToHost, ctx->compute);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->compute);
+    if (e != hipSuccess) return fail_hip(e, "light-cone result");
+    release();
+    if (hashes_out) fold_slots(ctx, generations, hashes_out);
+    ctx->epoch += (uint64_t)n;
+    return GOL_OK;
+}
+
+int gol_comm_abort(gol_ctx* ctx) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (!ctx->nccl) return GOL_OK;
+    if (int rc = bind(ctx)) return rc;
+    NCCL_CHECK(ctx, ncclCommAbort(ctx->nccl));
+    ctx->nccl = nullptr;
+    ctx->rank = 0;
+    ctx->nranks = 1;
+    return GOL_OK;
 }
 
 int gol_epoch(const gol_ctx* ctx, uint64_t* epoch) {

@@ -224,6 +224,30 @@ def simulation_params(cfg: dict) -> SimulationParams:
     )
 
 
+def crash_schedule(params: SimulationParams, generations: int, seed: int = 0) -> list[tuple[int, int]]:
+    """Injected crashes in generations, from the reference's wall-clock
+    schedule (BoardCreator.scala:97-102,107-108): NextStep fires at
+    start-delay + k * tick and advances to epoch k + 1; crashIfIMay fires at
+    errors.delay + i * errors.every and crashes a random child while fewer than
+    max-crashes have been crashed.  Crash i therefore lands after epoch
+    floor((delay + i * every - start) / tick) + 1.  Each entry is
+    (generation, pick): pick is the seeded stand-in for
+    Random.nextInt(children.size) (BoardCreator.scala:91-95) -- the victim is
+    live shard `pick % live_count`."""
+    import random
+    rng = random.Random(seed)
+    out = []
+    for i in range(params.max_number_of_crashes):
+        t = params.first_error_after_ms + i * params.error_every_ms
+        if t < params.start_delay_ms:
+            continue
+        g = (t - params.start_delay_ms) // params.tick_ms + 1
+        if g > generations:
+            break
+        out.append((int(g), rng.randrange(1 << 30)))
+    return out
+
+
 def iter_positions(cells: np.ndarray) -> Iterable[tuple[Position, bool]]:
     """(position, state) pairs in generateAllCoordinates order -- the payload
     of the reference's CellStateMsg stream for one epoch."""

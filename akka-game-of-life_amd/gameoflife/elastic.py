@@ -1,27 +1,36 @@
-"""Cross-process fault path: backends as processes, one lost mid-run.
+"""Cross-process fault path: backends as processes, lost ones re-spawned alone.
 
 Reference behaviour (BASELINE.json config 5): a
-backend JVM dies (Ctrl-C in ``README.md:12``), the cluster downs it after 1 s
-(``application.conf:23``), DeathWatch reports each of its cells
-``Terminated`` and ``BoardCreator.onCellTermination`` re-deploys them on a
-surviving backend, where they replay from the epoch-0 state and their
-neighbours' never-pruned histories (``BoardCreator.scala:120-154``,
-``CellActor.scala:34,71-74,86``).
+backend JVM dies (Ctrl-C in ``README.md:12``) or a cell is crashed on purpose
+(``crashIfIMay``, every ``errors.every`` after ``errors.delay`` up to
+``max-crashes``, ``BoardCreator.scala:97-102,108``).  DeathWatch reports the
+cell ``Terminated`` and ``BoardCreator.onCellTermination`` re-deploys only
+that cell, on a surviving node (``BoardCreator.scala:120-154``); it replays
+from its epoch-0 state using its neighbours' never-pruned histories
+(``CellActor.scala:34,71-74,86``) while every other cell keeps its state and
+simply waits for the answers it needs.
 
-Here a backend is one process per GPU that owns a row block (``GpuShard``:
-a libgol context, halo rows over RCCL).  Every ``ckpt_every`` generations
-each backend writes its shard checkpoint (``gol_checkpoint``) to a shared
-directory.  The ``Supervisor`` plays the frontend: it starts the backends,
-watches their progress, can inject a crash into one of them (the backend
-SIGKILLs itself once it has advanced to the given generation -- the
-analogue of the reference's injected ``DoCrashMsg``, ``BoardCreator.scala:
-97-102``, but the whole process is gone), notices the loss, stops the rest
-(their RCCL ring is broken), and re-deploys the whole board on the
-survivors: the new row
-blocks of the smaller decomposition are assembled from the last complete
-checkpoint written by the old one, and the lost generations are replayed.
-Generations are a pure function of that checkpoint, so the per-generation
-state hashes equal those of an uninterrupted run.
+Here a backend is one process per GPU owning a row block (``GpuShard``: a
+libgol context, halo rows over RCCL).  Every ``ckpt_every`` generations each
+backend writes its shard checkpoint (``gol_checkpoint``) to a shared
+directory.  The ``Supervisor`` plays the frontend: it starts the backends and
+releases them chunk by chunk (a backend only enters the next ring exchange
+when the supervisor says go, so when one dies the others are parked between
+steps, never inside a collective).  When a backend is lost at epoch t:
+
+* its row block is re-spawned on a surviving GPU -- the backend whose rows
+  are adjacent to it absorbs it: it restores the lost block's checkpoint at
+  epoch c <= t, takes the t - c rows above and below it at epoch c from the
+  neighbours' checkpoint files (the light cone), and replays the block alone
+  to epoch t (``gol_replay``), then owns both blocks as one context;
+* nobody else rolls back: the survivors stay at epoch t;
+* the ring is rebuilt around the merged backend (``gol_comm_abort`` +
+  ``gol_comm_init`` with a new unique id) and the run continues.
+
+The replayed block's per-generation partial hashes are checked against the
+global hashes recorded before the loss minus the survivors' partials.  If the
+last backend dies, a fresh one restores the whole board from the checkpoint
+files and replays it to epoch t the same way.
 
 Each backend is ``python -m gameoflife.elastic worker ...``; the shard
 implementation is pluggable (``--shard module:Class``) so the CPU tests can
@@ -101,75 +110,138 @@ def _shard_files(ckpt_dir: str, epoch: int) -> list[tuple[int, int, str]]:
     return sorted(out)
 
 
+def _covers(files: list[tuple[int, int, str]], lo: int, hi: int) -> bool:
+    """Do the files' row blocks cover [lo, hi)?  Blocks may overlap: every
+    file of one epoch holds that epoch's true rows (the board at an epoch is a
+    pure function of the initial board), whichever decomposition wrote it."""
+    nxt = lo
+    for row0, rows, _ in sorted(files):
+        if row0 > nxt:
+            break
+        nxt = max(nxt, row0 + rows)
+    return nxt >= hi
+
+
 def complete_epochs(ckpt_dir: str, height: int) -> list[int]:
-    """Checkpoint epochs whose shard files tile rows [0, height) exactly."""
+    """Checkpoint epochs whose shard files cover rows [0, height)."""
     out = []
     for name in sorted(os.listdir(ckpt_dir)) if os.path.isdir(ckpt_dir) else []:
-        if not name.startswith("e"):
-            continue
-        epoch, nxt = int(name[1:]), 0
-        for row0, rows, _ in _shard_files(ckpt_dir, epoch):
-            if row0 != nxt:
-                break
-            nxt = row0 + rows
-        if nxt == height:
-            out.append(epoch)
+        if name.startswith("e") and _covers(_shard_files(ckpt_dir, int(name[1:])), 0, height):
+            out.append(int(name[1:]))
     return out
+
+
+def covering_epochs(ckpt_dir: str, lo: int, hi: int) -> list[int]:
+    """Checkpoint epochs whose files cover rows [lo, hi)."""
+    out = []
+    for name in sorted(os.listdir(ckpt_dir)) if os.path.isdir(ckpt_dir) else []:
+        if name.startswith("e") and _covers(_shard_files(ckpt_dir, int(name[1:])), lo, hi):
+            out.append(int(name[1:]))
+    return out
+
+
+def blob_rows(blobs, indices) -> np.ndarray:
+    """Rows `indices` (global row numbers) cut from checkpoint blobs of one
+    epoch (any decomposition; blocks may overlap)."""
+    idx = np.asarray(list(indices), dtype=np.int64)
+    out, done = None, np.zeros(idx.size, dtype=bool)
+    for blob in blobs:
+        h, data = parse_checkpoint(blob)
+        f0, fn = h["row0"], h["rows"]
+        if out is None:
+            out = np.zeros((idx.size, data.shape[1]), dtype=np.uint32)
+        sel = (~done) & (idx >= f0) & (idx < f0 + fn)
+        out[sel] = data[idx[sel] - f0]
+        done |= sel
+    if out is None or not done.all():
+        raise ValueError(f"checkpoints do not hold rows {idx[~done][:4].tolist()}...")
+    return out
+
+
+def checkpoint_rows(ckpt_dir: str, epoch: int, indices) -> np.ndarray:
+    """Rows `indices` (global row numbers in [0, height)) of the board at
+    `epoch`, cut from whatever shard files hold them."""
+    idx = np.asarray(list(indices), dtype=np.int64)
+    blobs = []
+    for f0, fn, path in _shard_files(ckpt_dir, epoch):
+        if ((idx >= f0) & (idx < f0 + fn)).any():
+            with open(path, "rb") as f:
+                blobs.append(f.read())
+    try:
+        return blob_rows(blobs, idx)
+    except ValueError as e:
+        raise FileNotFoundError(f"epoch {epoch}: {e}") from None
 
 
 def assemble_checkpoint(ckpt_dir: str, epoch: int, row0: int, rows: int) -> bytes:
     """Checkpoint blob for rows [row0, row0 + rows) at `epoch`, cut from the
     shard files of whatever decomposition wrote that epoch."""
-    parts, header = [], None
-    for f0, fn, path in _shard_files(ckpt_dir, epoch):
-        lo, hi = max(row0, f0), min(row0 + rows, f0 + fn)
-        if lo >= hi:
+    files = _shard_files(ckpt_dir, epoch)
+    if not files:
+        raise FileNotFoundError(f"no checkpoint at epoch {epoch}")
+    with open(files[0][2], "rb") as f:
+        header, _ = parse_checkpoint(f.read())
+    packed = checkpoint_rows(ckpt_dir, epoch, range(row0, row0 + rows))
+    return make_checkpoint(dict(header, row0=row0, rows=rows, epoch=epoch), packed)
+
+
+def light_cone_from(get_rows, row0: int, rows: int, depth: int, height: int, torus: bool,
+                    wwords: int) -> tuple[np.ndarray, np.ndarray]:
+    """The `depth` rows above row0 and below row0 + rows (mod the height on a
+    torus; dead rows beyond a clipped board's edge), read with
+    get_rows(global row indices): with the block's own rows they fix the block
+    for `depth` generations (gol_replay)."""
+    res = []
+    for idx in ([row0 - depth + k for k in range(depth)], [row0 + rows + k for k in range(depth)]):
+        if torus:
+            res.append(get_rows([i % height for i in idx]) if idx else np.zeros((0, wwords), np.uint32))
             continue
-        with open(path, "rb") as f:
-            h, data = parse_checkpoint(f.read())
-        header = h
-        parts.append((lo, data[lo - f0:hi - f0]))
-    if header is None:
-        raise FileNotFoundError(f"no checkpoint rows for [{row0}, {row0 + rows}) at epoch {epoch}")
-    parts.sort(key=lambda p: p[0])
-    packed = np.vstack([p[1] for p in parts])
-    if packed.shape[0] != rows:
-        raise ValueError(f"checkpoint at epoch {epoch} covers {packed.shape[0]} of {rows} rows")
-    header = dict(header, row0=row0, rows=rows)
-    return make_checkpoint(header, packed)
+        a = np.zeros((len(idx), wwords), dtype=np.uint32)
+        inside = [k for k, i in enumerate(idx) if 0 <= i < height]
+        if inside:
+            a[inside] = get_rows([idx[k] for k in inside])
+        res.append(a)
+    return res[0], res[1]
+
+
+def light_cone(ckpt_dir: str, epoch: int, row0: int, rows: int, depth: int, height: int,
+               torus: bool) -> tuple[np.ndarray, np.ndarray]:
+    """light_cone_from the checkpoint files of `epoch`."""
+    files = _shard_files(ckpt_dir, epoch)
+    if not files:
+        raise FileNotFoundError(f"no checkpoint at epoch {epoch}")
+    with open(files[0][2], "rb") as f:
+        wwords = parse_checkpoint(f.read())[0]["wwords"]
+    return light_cone_from(lambda idx: checkpoint_rows(ckpt_dir, epoch, idx), row0, rows, depth, height, torus,
+                           wwords)
 
 
 # ----------------------------------------------------------- shards
 
 class GpuShard:
     """The product backend: one libgol context on one GPU; halo rows and the
-    per-generation hash reduction over RCCL (rank 0 publishes the unique id
-    in the attempt directory)."""
+    per-generation hash reduction over RCCL (the ring's rank 0 publishes the
+    unique id in the ring directory)."""
 
-    def __init__(self, width, height, row0, rows, rank, world, attempt_dir, topology="torus",
-                 rule="life", device=None):
-        from . import _native as N
+    def __init__(self, width, height, row0, rows, topology="torus", rule="life", device=0):
         from .engine import GolEngine
-        ndev = N.device_count()
+        self.width, self.height, self.row0, self.rows = width, height, row0, rows
+        self.topology, self.rule, self.device = topology, rule, device
+        self.world = 1
+        self.eng = GolEngine(width, height, topology=topology, rule=rule, device=device, row0=row0, rows=rows)
+
+    def join(self, ring_dir, rank, world):
+        """Join the ring `ring_dir` as rank/world (a 1-rank ring needs none)."""
+        from . import _native as N
         self.world = world
-        self.eng = GolEngine(width, height, topology=topology, rule=rule,
-                             device=rank % ndev if device is None else device, row0=row0, rows=rows)
-        if world > 1:
-            uid_path = os.path.join(attempt_dir, "rccl_uid")
-            if rank == 0:
-                uid = N.unique_id()
-                tmp = uid_path + ".tmp"
-                with open(tmp, "wb") as f:
-                    f.write(uid)
-                os.replace(tmp, uid_path)
-            else:
-                deadline = time.time() + 120
-                while not os.path.exists(uid_path):
-                    if time.time() > deadline:
-                        raise TimeoutError("no RCCL unique id from rank 0")
-                    time.sleep(0.05)
-                uid = open(uid_path, "rb").read()
-            self.eng.comm_init(uid, rank, world)
+        if world == 1:
+            return
+        uid = _ring_uid(ring_dir, rank, N.unique_id)
+        self.eng.comm_init(uid, rank, world)
+
+    def leave(self):
+        self.eng.comm_abort()
+        self.world = 1
 
     def seed(self, seed):
         self.eng.seed(seed)
@@ -181,11 +253,42 @@ class GpuShard:
         return self.eng.checkpoint()
 
     def step(self, n):
+        """-> (global per-generation hashes, this shard's partials)."""
         part = self.eng.step(n, hashes=True)
-        return self.eng.allreduce_u64(part) if self.world > 1 else part
+        return (self.eng.allreduce_u64(part) if self.world > 1 else part), part
 
     def close(self):
         self.eng.close()
+
+    @staticmethod
+    def replay_block(width, height, blob, above, below, depth, topology="torus", rule="life", device=0):
+        """Light-cone replay of a lost block (gol_replay) on `device`:
+        -> (the block's rows `depth` generations later, its partial hashes)."""
+        from .engine import GolEngine
+        h, _ = parse_checkpoint(blob)
+        with GolEngine(width, height, topology=topology, rule=rule, device=device, row0=h["row0"],
+                       rows=h["rows"]) as e:
+            e.restore(blob)
+            hs = e.replay(depth, above, below) if depth else np.zeros(0, dtype=np.uint64)
+            return e.snapshot(), hs
+
+
+def _ring_uid(ring_dir, rank, make_uid) -> bytes:
+    """Rank 0 publishes the ring's unique id; the others wait for it."""
+    path = os.path.join(ring_dir, "rccl_uid")
+    if rank == 0:
+        uid = make_uid()
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return uid
+    deadline = time.time() + 120
+    while not os.path.exists(path):
+        if time.time() > deadline:
+            raise TimeoutError("no ring unique id from rank 0")
+        time.sleep(0.02)
+    return open(path, "rb").read()
 
 
 def _load_class(spec: str):
@@ -193,143 +296,322 @@ def _load_class(spec: str):
     return getattr(importlib.import_module(mod), cls)
 
 
+def _write_json(path, obj):
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+
+
+def _read_json(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
 # ----------------------------------------------------------- backend process
 
 def worker_main(a) -> int:
-    row0, rows = shard_rows_py(a.height, a.rank, a.world)
-    shard = _load_class(a.shard)(a.width, a.height, row0, rows, a.rank, a.world, a.attempt_dir,
-                                 topology=a.topology, rule=a.rule)
-    progress = os.path.join(a.attempt_dir, f"progress_r{a.rank}")
-    hashes = open(os.path.join(a.attempt_dir, "hashes.txt"), "a") if a.rank == 0 else None
+    """One backend: runs the supervisor's commands (cmd/w<id>.<seq>, JSON)
+    and reports after each one (status/w<id>)."""
+    cls = _load_class(a.shard)
+    torus = a.topology == "torus"
+    row0, rows = a.row0, a.rows
+    shard = cls(a.width, a.height, row0, rows, topology=a.topology, rule=a.rule, device=a.device)
+    hashes = open(os.path.join(a.workdir, "hashes.txt"), "a")
+    partials = open(os.path.join(a.workdir, f"partials_w{a.wid}.txt"), "a")
+    status = os.path.join(a.workdir, "status", f"w{a.wid}")
+    rank, world = a.rank, a.world
+    extra = {}
 
-    def report(epoch):
-        with open(progress + ".tmp", "w") as f:
-            f.write(str(epoch))
-        os.replace(progress + ".tmp", progress)
+    def report(seq, epoch):
+        _write_json(status, dict(seq=seq, epoch=epoch, row0=row0, rows=rows, pid=os.getpid(), **extra))
 
-    if a.start == 0:
+    if a.resume < 0:
         shard.seed(a.seed)
+        epoch = 0
         write_shard_checkpoint(a.ckpt_dir, shard.checkpoint())
-    else:
-        shard.restore(assemble_checkpoint(a.ckpt_dir, a.start, row0, rows))
-    epoch = a.start
-    report(epoch)
-    while epoch < a.gens:
-        n = min(a.chunk, a.every - epoch % a.every, a.gens - epoch)
-        hs = shard.step(n)
-        if hashes:
-            for k, h in enumerate(hs):
-                hashes.write(f"{epoch + k + 1} {int(h)}\n")
-            hashes.flush()
-        epoch += n
-        if 0 <= a.crash_at <= epoch:  # injected crash: the process dies here
-            os.kill(os.getpid(), signal.SIGKILL)
-        if epoch % a.every == 0:
-            write_shard_checkpoint(a.ckpt_dir, shard.checkpoint())
-        report(epoch)
-    shard.close()
-    return 0
+    else:  # a re-spawned board: restore epoch c, replay to the target alone
+        blob = assemble_checkpoint(a.ckpt_dir, a.resume, row0, rows)
+        d = a.target - a.resume
+        up, dn = light_cone(a.ckpt_dir, a.resume, row0, rows, d, a.height, torus)
+        cur, hs = cls.replay_block(a.width, a.height, blob, up, dn, d, topology=a.topology, rule=a.rule,
+                                   device=a.device)
+        h, _ = parse_checkpoint(blob)
+        shard.restore(make_checkpoint(dict(h, epoch=a.target), cur))
+        epoch = a.target
+        extra["replayed"] = {"from": a.resume, "to": a.target, "partials": [str(int(x)) for x in hs]}
+    shard.join(a.ring_dir, rank, world)
+    report(0, epoch)
+    seq = 0
+    while True:
+        seq += 1
+        path = os.path.join(a.workdir, "cmd", f"w{a.wid}.{seq}")
+        while not os.path.exists(path):
+            time.sleep(0.005)
+        cmd = _read_json(path)
+        while cmd is None:
+            time.sleep(0.005)
+            cmd = _read_json(path)
+        op = cmd["op"]
+        if op == "stop":
+            shard.close()
+            report(seq, epoch)
+            return 0
+        if op == "go":
+            n = cmd["n"]
+            glob, part = shard.step(n)
+            if rank == 0:
+                hashes.write("".join(f"{epoch + k + 1} {int(x)}\n" for k, x in enumerate(glob)))
+                hashes.flush()
+            partials.write("".join(f"{epoch + k + 1} {row0} {rows} {int(x)}\n" for k, x in enumerate(part)))
+            partials.flush()
+            epoch += n
+            if cmd.get("crash"):  # injected crash (DoCrashMsg): the process dies here
+                os.kill(os.getpid(), signal.SIGKILL)
+            if epoch % a.every == 0:
+                write_shard_checkpoint(a.ckpt_dir, shard.checkpoint())
+        elif op == "absorb":
+            # re-spawn the lost block next to this one: replay it alone from
+            # its checkpoint with the light cone, then own both blocks
+            lo, n_lost, c = cmd["row0"], cmd["rows"], cmd["ckpt_epoch"]
+            d = epoch - c
+            blob = assemble_checkpoint(a.ckpt_dir, c, lo, n_lost)
+            up, dn = light_cone(a.ckpt_dir, c, lo, n_lost, d, a.height, torus)
+            lost_rows, hs = cls.replay_block(a.width, a.height, blob, up, dn, d, topology=a.topology,
+                                             rule=a.rule, device=a.device)
+            mine_h, mine = parse_checkpoint(shard.checkpoint())
+            shard.leave()
+            shard.close()
+            if lo + n_lost == row0:
+                merged, row0 = np.vstack([lost_rows, mine]), lo
+            elif row0 + rows == lo:
+                merged = np.vstack([mine, lost_rows])
+            else:
+                raise ValueError(f"block [{lo}, {lo + n_lost}) is not adjacent to [{row0}, {row0 + rows})")
+            rows += n_lost
+            shard = cls(a.width, a.height, row0, rows, topology=a.topology, rule=a.rule, device=a.device)
+            shard.restore(make_checkpoint(dict(mine_h, row0=row0, rows=rows, epoch=epoch), merged))
+            extra["replayed"] = {"from": c, "to": epoch, "row0": lo, "rows": n_lost,
+                                 "partials": [str(int(x)) for x in hs]}
+            world = 1
+        elif op == "rejoin":
+            shard.leave()
+            rank, world = cmd["rank"], cmd["world"]
+            shard.join(cmd["ring"], rank, world)
+        report(seq, epoch)
 
 
 # ----------------------------------------------------------- supervisor
 
+class _Worker:
+    def __init__(self, wid, proc, row0, rows, rank, device):
+        self.wid, self.proc, self.row0, self.rows, self.rank, self.device = wid, proc, row0, rows, rank, device
+        self.seq = 0
+
+
 class Supervisor:
-    """The frontend's role: deploy the board on `world` backends, optionally
-    crash backend `kill = (rank, generation)` once it has advanced that far
-    (before it writes a checkpoint there), and on
-    any backend loss re-deploy on the survivors from the last complete
-    checkpoint.  `hashes()` maps every generation to the global state hash
-    (replayed generations overwrite the lost run's)."""
+    """The frontend's role: deploy the board on `world` backends, release them
+    chunk by chunk, inject crashes, and re-spawn each lost block next to a
+    survivor (lost-shard-only light-cone recovery, module docstring).
+
+    crashes: [(generation, pick)] -- after `generation`, live backend number
+    pick % live (in row order) dies (board.crash_schedule turns the
+    reference's errors.delay / errors.every / max-crashes into this);
+    kill = (rank, generation) is the one-crash shorthand.  `hashes()` maps
+    every generation to the global state hash."""
 
     def __init__(self, width, height, gens, world, workdir, ckpt_every=10, seed=0x5EED,
                  topology="torus", rule="life", shard="gameoflife.elastic:GpuShard", chunk=1,
-                 kill=None, timeout=600.0, env=None):
+                 kill=None, crashes=None, timeout=600.0, env=None, devices=None):
         self.width, self.height, self.gens, self.world = width, height, gens, world
         self.workdir, self.every, self.seed = workdir, ckpt_every, seed
         self.topology, self.rule, self.shard, self.chunk = topology, rule, shard, chunk
-        self.kill = kill  # (rank, epoch) or None
+        self.crashes = sorted(crashes or ([] if kill is None else [(kill[1], kill[0])]))
         self.timeout = timeout
+        self.devices = list(devices) if devices is not None else None
         self.env = dict(os.environ if env is None else env)
         pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         self.env["PYTHONPATH"] = os.pathsep.join([pkg] + [p for p in self.env.get("PYTHONPATH", "").split(
             os.pathsep) if p])
         self.ckpt_dir = os.path.join(workdir, "ckpt")
         self.events: list[dict] = []
-        self.attempts: list[str] = []
+        self.workers: list[_Worker] = []
+        self.next_wid = 0
+        self.ring = 0
+        self.deadline = 0.0
 
-    def _launch(self, attempt, world, start, crash=None):
-        d = os.path.join(self.workdir, f"attempt{attempt}")
+    # -- plumbing -----------------------------------------------------------
+    def _device_count(self):
+        if self.devices is None:
+            try:
+                from . import _native as N
+                self.devices = list(range(max(1, N.device_count())))
+            except Exception:
+                self.devices = [0]
+        return self.devices
+
+    def _ring_dir(self):
+        d = os.path.join(self.workdir, f"ring{self.ring}")
         os.makedirs(d, exist_ok=True)
-        self.attempts.append(d)
-        procs = []
-        for r in range(world):
-            cmd = [sys.executable, "-m", "gameoflife.elastic", "worker",
-                   "--width", str(self.width), "--height", str(self.height), "--gens", str(self.gens),
-                   "--every", str(self.every), "--seed", str(self.seed), "--rank", str(r),
-                   "--world", str(world), "--start", str(start), "--ckpt-dir", self.ckpt_dir,
-                   "--attempt-dir", d, "--topology", self.topology, "--rule", self.rule,
-                   "--shard", self.shard, "--chunk", str(self.chunk),
-                   "--crash-at", str(crash[1] if crash and crash[0] == r else -1)]
-            log = open(os.path.join(d, f"worker_r{r}.log"), "w")
-            procs.append(subprocess.Popen(cmd, env=self.env, stdout=log, stderr=subprocess.STDOUT))
-        self.events.append({"event": "deploy", "attempt": attempt, "world": world, "start": start})
-        return d, procs
+        return d
 
-    @staticmethod
-    def _progress(d, r):
-        try:
-            return int(open(os.path.join(d, f"progress_r{r}")).read() or -1)
-        except (OSError, ValueError):
-            return -1
+    def _spawn(self, row0, rows, rank, world, device, resume=-1, target=-1):
+        wid = self.next_wid
+        self.next_wid += 1
+        cmd = [sys.executable, "-m", "gameoflife.elastic", "worker",
+               "--wid", str(wid), "--width", str(self.width), "--height", str(self.height),
+               "--every", str(self.every), "--seed", str(self.seed), "--row0", str(row0), "--rows", str(rows),
+               "--rank", str(rank), "--world", str(world), "--device", str(device),
+               "--resume", str(resume), "--target", str(target), "--ring-dir", self._ring_dir(),
+               "--workdir", self.workdir, "--ckpt-dir", self.ckpt_dir, "--topology", self.topology,
+               "--rule", self.rule, "--shard", self.shard]
+        log = open(os.path.join(self.workdir, "logs", f"worker_w{wid}.log"), "w")
+        proc = subprocess.Popen(cmd, env=self.env, stdout=log, stderr=subprocess.STDOUT)
+        w = _Worker(wid, proc, row0, rows, rank, device)
+        self.workers.append(w)
+        return w
 
+    def _send(self, w, cmd):
+        w.seq += 1
+        _write_json(os.path.join(self.workdir, "cmd", f"w{w.wid}.{w.seq}"), cmd)
+
+    def _wait(self, ws):
+        """Wait until every worker in `ws` has reported its last command, or
+        one of them died.  -> (statuses by wid, dead workers)."""
+        while True:
+            if time.time() > self.deadline:
+                raise TimeoutError("elastic run exceeded its time limit")
+            dead = [w for w in ws if w.proc.poll() not in (None, 0)]
+            st = {w.wid: _read_json(os.path.join(self.workdir, "status", f"w{w.wid}")) for w in ws}
+            done = all(st[w.wid] is not None and st[w.wid]["seq"] >= w.seq for w in ws if w not in dead)
+            if done:
+                return st, dead
+            time.sleep(0.01)
+
+    def _rering(self):
+        """Renumber the live backends in row order and rebuild the ring."""
+        self.workers.sort(key=lambda w: w.row0)
+        self.ring += 1
+        ring = self._ring_dir()
+        for r, w in enumerate(self.workers):
+            w.rank = r
+            self._send(w, {"op": "rejoin", "ring": ring, "rank": r, "world": len(self.workers)})
+        st, dead = self._wait(self.workers)
+        if dead:
+            raise RuntimeError("a backend died while the ring was rebuilt")
+        return st
+
+    # -- recovery -----------------------------------------------------------
+    def _recover(self, lost: list[_Worker], epoch: int):
+        for w in lost:
+            self.workers.remove(w)
+        for w in sorted(lost, key=lambda w: w.row0):
+            eps = [e for e in covering_epochs(self.ckpt_dir, w.row0, w.row0 + w.rows) if e <= epoch]
+            c = eps[-1]
+            ev = {"event": "lost", "worker": w.wid, "rows": [w.row0, w.row0 + w.rows], "epoch": epoch,
+                  "checkpoint_epoch": c, "replayed_generations": epoch - c}
+            above = [s for s in self.workers if s.row0 + s.rows == w.row0]
+            below = [s for s in self.workers if s.row0 == w.row0 + w.rows]
+            host = (above or below or [None])[0]
+            if host is None:  # the last backend: a fresh one for the whole board
+                devs = self._device_count()
+                nw = self._spawn(0, self.height, 0, 1, devs[(w.device + 1) % len(devs)], resume=c, target=epoch)
+                st, dead = self._wait([nw])
+                if dead:
+                    raise RuntimeError("the re-spawned backend died")
+                ev.update(respawned_as=nw.wid, device=nw.device, new_world=1)
+                self._check_replay(st[nw.wid]["replayed"], epoch)
+            else:
+                self._send(host, {"op": "absorb", "row0": w.row0, "rows": w.rows, "ckpt_epoch": c})
+                st, dead = self._wait([host])
+                if dead:
+                    raise RuntimeError("the absorbing backend died")
+                host.row0, host.rows = st[host.wid]["row0"], st[host.wid]["rows"]
+                ev.update(absorbed_by=host.wid, device=host.device, new_world=len(self.workers))
+                self._check_replay(st[host.wid]["replayed"], epoch)
+            self.events.append(ev)
+        self._rering()
+
+    def _check_replay(self, rep, epoch):
+        """The replayed block's partial hashes must complete the global hashes
+        recorded before the loss (sum of the other blocks' partials + it)."""
+        part = self._partials()
+        glob = self.hashes()
+        lo, rows = rep.get("row0", 0), rep.get("rows", self.height)
+        for k, p in enumerate(rep["partials"]):
+            g = rep["from"] + k + 1
+            if g not in glob:
+                continue
+            others = sum(v for (r0, n), v in part.get(g, {}).items() if r0 + n <= lo or r0 >= lo + rows)
+            if (others + int(p)) % (1 << 64) != glob[g]:
+                raise AssertionError(f"replayed partial of generation {g} does not complete the global hash")
+
+    def _partials(self) -> dict:
+        out: dict = {}
+        logs = os.path.join(self.workdir)
+        for name in os.listdir(logs):
+            if name.startswith("partials_w"):
+                for line in open(os.path.join(logs, name)):
+                    g, r0, n, h = (int(x) for x in line.split())
+                    out.setdefault(g, {})[(r0, n)] = h
+        return out
+
+    # -- main loop ----------------------------------------------------------
     def run(self) -> dict:
-        os.makedirs(self.workdir, exist_ok=True)
-        deadline = time.time() + self.timeout
-        world, start, attempt = self.world, 0, 0
-        d, procs = self._launch(attempt, world, start, crash=self.kill)
-        if self.kill:
-            self.events.append({"event": "inject-crash", "rank": self.kill[0], "generation": self.kill[1]})
+        for sub in ("cmd", "status", "logs"):
+            os.makedirs(os.path.join(self.workdir, sub), exist_ok=True)
+        self.deadline = time.time() + self.timeout
+        devs = self._device_count()
+        for r in range(self.world):
+            row0, rows = shard_rows_py(self.height, r, self.world)
+            self._spawn(row0, rows, r, self.world, devs[r % len(devs)])
+        self.events.append({"event": "deploy", "world": self.world})
+        pending = list(self.crashes)
         try:
-            while True:
-                if time.time() > deadline:
-                    raise TimeoutError("elastic run exceeded its time limit")
-                codes = [p.poll() for p in procs]
-                if all(c == 0 for c in codes):
-                    break
-                if any(c not in (None, 0) for c in codes):
-                    lost = [r for r, c in enumerate(codes) if c not in (None, 0)]
-                    progress = {r: self._progress(d, r) for r in range(len(procs))}
-                    for p in procs:  # the ring is broken: stop the others too
-                        if p.poll() is None:
-                            p.send_signal(signal.SIGKILL)
-                    for p in procs:
-                        p.wait()
-                    epochs = complete_epochs(self.ckpt_dir, self.height)
-                    if not epochs:
-                        raise RuntimeError("backend lost before the first checkpoint")
-                    start = epochs[-1]
-                    world = max(1, world - len(lost))
-                    attempt += 1
-                    self.events.append({"event": "lost", "ranks": lost, "progress": progress,
-                                        "restart_epoch": start, "new_world": world})
-                    d, procs = self._launch(attempt, world, start)
-                    continue
-                time.sleep(0.02)
+            st, dead = self._wait(self.workers)
+            if dead:
+                raise RuntimeError("a backend died during deployment")
+            epoch = 0
+            while epoch < self.gens:
+                while pending and pending[0][0] <= epoch:
+                    pending.pop(0)
+                n = min(self.chunk, self.every - epoch % self.every, self.gens - epoch)
+                victim = None
+                if pending and epoch + n >= pending[0][0]:
+                    n = pending[0][0] - epoch
+                    victim = sorted(self.workers, key=lambda w: w.row0)[pending[0][1] % len(self.workers)]
+                    self.events.append({"event": "inject-crash", "worker": victim.wid, "generation": epoch + n})
+                for w in self.workers:
+                    self._send(w, {"op": "go", "n": n, "crash": w is victim})
+                st, dead = self._wait(self.workers)
+                for w in dead:
+                    w.proc.wait()
+                epoch += n
+                if dead:
+                    self._recover(dead, epoch)
+            for w in self.workers:
+                self._send(w, {"op": "stop"})
+            self._wait(self.workers)
+            for w in self.workers:
+                if w.proc.wait(timeout=60) != 0:
+                    raise RuntimeError(f"backend w{w.wid} exited with {w.proc.returncode}")
         finally:
-            for p in procs:
-                if p.poll() is None:
-                    p.send_signal(signal.SIGKILL)
-                    p.wait()
+            for w in self.workers:
+                if w.proc.poll() is None:
+                    w.proc.send_signal(signal.SIGKILL)
+                    w.proc.wait()
         return self.hashes()
 
     def hashes(self) -> dict:
         out = {}
-        for d in self.attempts:
-            path = os.path.join(d, "hashes.txt")
-            if os.path.exists(path):
-                for line in open(path):
-                    e, h = line.split()
-                    out[int(e)] = int(h)
+        path = os.path.join(self.workdir, "hashes.txt")
+        if os.path.exists(path):
+            for line in open(path):
+                e, h = line.split()
+                out[int(e)] = int(h)
         return out
 
 
@@ -339,13 +621,12 @@ def _parser():
     ap = argparse.ArgumentParser(prog="python -m gameoflife.elastic")
     sub = ap.add_subparsers(dest="cmd", required=True)
     w = sub.add_parser("worker", help="one backend process (started by the supervisor)")
-    for name, typ in [("--width", int), ("--height", int), ("--gens", int), ("--every", int),
-                      ("--seed", int), ("--rank", int), ("--world", int), ("--start", int),
-                      ("--chunk", int), ("--crash-at", int)]:
-        w.add_argument(name, type=typ, required=True)
-    for name in ("--ckpt-dir", "--attempt-dir", "--topology", "--rule", "--shard"):
+    for name in ("--wid", "--width", "--height", "--every", "--seed", "--row0", "--rows", "--rank", "--world",
+                 "--device", "--resume", "--target"):
+        w.add_argument(name, type=int, required=True)
+    for name in ("--ring-dir", "--workdir", "--ckpt-dir", "--topology", "--rule", "--shard"):
         w.add_argument(name, required=True)
-    dm = sub.add_parser("demo", help="BASELINE.json config 5: kill one backend mid-run")
+    dm = sub.add_parser("demo", help="BASELINE.json config 5: kill backends mid-run")
     dm.add_argument("--width", type=int, default=262144)
     dm.add_argument("--height", type=int, default=262144)
     dm.add_argument("--gens", type=int, default=50)

@@ -127,6 +127,23 @@ class GolEngine:
         arr = (ctypes.c_uint8 * N.GOL_UNIQUE_ID_BYTES).from_buffer_copy(uid)
         self._chk(N.lib.gol_comm_init(self._h, arr, rank, nranks))
 
+    def comm_abort(self) -> None:
+        """Leave the ring (gol_comm_abort); comm_init may join a new one."""
+        self._chk(N.lib.gol_comm_abort(self._h))
+
+    def replay(self, generations: int, above: np.ndarray, below: np.ndarray, hashes: bool = True):
+        """Light-cone replay (gol_replay): advance this shard `generations`
+        generations alone from the `generations` rows above and below it at
+        its current epoch.  Returns the shard's per-generation partial hashes."""
+        a = np.ascontiguousarray(above, dtype=np.uint32)
+        b = np.ascontiguousarray(below, dtype=np.uint32)
+        if a.shape != (generations, self.wwords) or b.shape != a.shape:
+            raise ValueError(f"light-cone rows must be ({generations}, {self.wwords}) arrays")
+        out = np.zeros(generations, dtype=np.uint64) if hashes else None
+        self._chk(N.lib.gol_replay(self._h, generations, a.ctypes.data_as(N._u32p), b.ctypes.data_as(N._u32p),
+                                   self.wwords, out.ctypes.data_as(N._u64p) if hashes else None))
+        return out
+
     def allreduce_u64(self, values: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(values, dtype=np.uint64).copy()
         self._chk(N.lib.gol_comm_allreduce_u64(self._h, v.ctypes.data_as(N._u64p), v.size))

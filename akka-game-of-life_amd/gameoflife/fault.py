@@ -12,13 +12,18 @@ Reference behaviour:
 Here a shard (a row block in HBM) is the unit that dies.  Every
 ``checkpoint_every`` generations all shards save a consistent checkpoint
 (``gol_checkpoint``: epoch + packed rows) to host memory (optionally also to
-files).  When a shard is lost the group is rebuilt with a new context for the
-dead rows -- on any surviving GPU, possibly next to a shard it already hosts
--- every shard rolls back to the last checkpoint (global rollback; the
-counter-based board seed also allows regenerating epoch 0 as the reference
-does), and the lost generations are replayed.  Generations are a pure
-function of the checkpoint, so the per-generation hashes equal those of an
-uninterrupted run.
+files).  When a shard is lost at epoch t, a new context for its rows is
+created on a surviving GPU (possibly next to a shard it already hosts), it
+restores its own checkpoint of epoch c, takes the t - c rows above and below
+it at epoch c from its neighbours' checkpoints (the light cone) and replays
+alone to epoch t (``gol_replay``, ``respawn``); the surviving shards keep
+their state and wait, as the reference's surviving cells do.  Then the group
+is rebuilt and the run continues.  (``respawn(..., mode="rollback")`` is the
+older global rollback: every shard restores epoch c and the group replays.)
+``run(generations, crashes)`` injects crashes on a schedule (``crash_schedule``
+of the reference's errors.delay / errors.every / max-crashes keys).
+Generations are a pure function of the checkpoint, so the per-generation
+hashes equal those of an uninterrupted run.
 """
 from __future__ import annotations
 
@@ -26,6 +31,7 @@ import os
 
 import numpy as np
 
+from .elastic import blob_rows, light_cone_from
 from .engine import GolEngine, ShardGroup
 from .shard import shard_rows_py
 
@@ -101,33 +107,67 @@ class ShardedSimulation:
         self.group = None
         self.events.append(f"kill shard {k} @{self.epoch}")
 
-    def respawn(self, k: int, device: int | None = None) -> list[int]:
-        """Re-spawn shard k on `device` (default: the next surviving device),
-        roll every shard back to the last checkpoint and replay to the epoch
-        reached before the failure.  Returns the replayed hashes."""
+    def _checkpoint_blobs(self) -> list[bytes]:
+        if not self.checkpoint_dir:
+            return self.ckpt
+        blobs = []  # survive the loss of host memory too
+        for j in range(self.n):
+            with open(os.path.join(self.checkpoint_dir, f"shard{j}.ckpt"), "rb") as f:
+                blobs.append(f.read())
+        return blobs
+
+    def respawn(self, k: int, device: int | None = None, mode: str = "light-cone") -> list[int]:
+        """Re-spawn shard k on `device` (default: the next surviving device).
+
+        light-cone: shard k restores its checkpoint (epoch c) and replays the
+        lost generations c+1..epoch alone from its neighbours' checkpoint rows
+        (gol_replay); the other shards keep their state.  Returns shard k's
+        replayed per-generation partial hashes.
+        rollback: every shard restores epoch c and the group replays; returns
+        the replayed global hashes, checked against the lost ones."""
         if device is None:
             alive = [d for d in self.devices if d != self.placement[k]] or self.devices
             device = alive[0]
         self.placement[k] = device
         self.shards[k] = self._make(k, device)
-        blobs = self.ckpt
-        if self.checkpoint_dir:  # survive the loss of host memory too
-            blobs = []
-            for j in range(self.n):
-                with open(os.path.join(self.checkpoint_dir, f"shard{j}.ckpt"), "rb") as f:
-                    blobs.append(f.read())
-        for s, blob in zip(self.shards, blobs):
-            s.restore(blob)
-        target = self.epoch
-        self.epoch = self.ckpt_epoch
-        lost = self.hashes[self.ckpt_epoch:]
-        del self.hashes[self.ckpt_epoch:]
+        blobs = self._checkpoint_blobs()
+        if mode == "rollback":
+            for s, blob in zip(self.shards, blobs):
+                s.restore(blob)
+            target = self.epoch
+            self.epoch = self.ckpt_epoch
+            lost = self.hashes[self.ckpt_epoch:]
+            del self.hashes[self.ckpt_epoch:]
+            self.group = ShardGroup(self.shards)
+            self.events.append(f"respawn shard {k} on device {device}, rollback to {self.ckpt_epoch}")
+            replayed = self.step(target - self.epoch) if target > self.epoch else []
+            if replayed != lost:
+                raise AssertionError("replayed generations differ from the lost ones")
+            return replayed
+        s = self.shards[k]
+        s.restore(blobs[k])
+        d = self.epoch - self.ckpt_epoch
+        up, dn = light_cone_from(lambda idx: blob_rows(blobs, idx), s.row0, s.rows, d, self.height,
+                                 self.topology == "torus", s.wwords)
+        part = [int(h) for h in s.replay(d, up, dn)] if d else []
         self.group = ShardGroup(self.shards)
-        self.events.append(f"respawn shard {k} on device {device}, rollback to {self.ckpt_epoch}")
-        replayed = self.step(target - self.epoch) if target > self.epoch else []
-        if replayed != lost:
-            raise AssertionError("replayed generations differ from the lost ones")
-        return replayed
+        self.events.append(f"respawn shard {k} on device {device}, light cone {self.ckpt_epoch}->{self.epoch}")
+        return part
+
+    def run(self, generations: int, crashes: list[tuple[int, int]] = ()) -> list[int]:
+        """Advance `generations`, crashing shard pick % n after each crash
+        generation (board.crash_schedule) and re-spawning it alone."""
+        out: list[int] = []
+        end = self.epoch + generations
+        for g, pick in sorted(crashes):
+            if g <= self.epoch or g > end:
+                continue
+            out.extend(self.step(g - self.epoch))
+            k = pick % self.n
+            self.kill(k)
+            self.respawn(k)
+        out.extend(self.step(end - self.epoch))
+        return out
 
     def snapshot(self) -> np.ndarray:
         return np.vstack([s.snapshot() for s in self.shards])

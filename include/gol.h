@@ -138,6 +138,23 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out);
  * capacity. */
 int gol_step_ex(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out, size_t hashes_capacity);
 
+/* Light-cone replay of a re-spawned shard, alone.  Replaces the reference's
+ * re-born cell catching up from its neighbours' never-pruned histories
+ * (BoardCreator.scala:138-154 re-deploys it, CellActor.scala:34,71-74,86 it
+ * replays epoch by epoch from their answers).  ctx holds its rows at epoch e
+ * (gol_restore of its own checkpoint); `above` holds the n = `generations`
+ * rows just above row0 and `below` the n rows just below row0 + rows, as they
+ * were at epoch e (global rows row0 - n .. row0 - 1 and row0 + rows ..
+ * row0 + rows + n - 1, modulo the height on a torus; dead rows beyond a
+ * clipped board's edge), row-major host rows `host_pitch_words` apart.  The
+ * block n rows deeper on each side fixes the shard's rows for n generations,
+ * so ctx advances n generations exactly as if its neighbours had been there,
+ * while they stay where they are.  hashes_out (nullable, n entries) receives
+ * the shard's per-generation partial hashes.  The context must not belong to
+ * a group or ring yet (GOL_ESTATE). */
+int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const uint32_t* below,
+               int64_t host_pitch_words, uint64_t* hashes_out);
+
 /* Current epoch (CellActor.scala:39 myCurrentEpoch). */
 int gol_epoch(const gol_ctx* ctx, uint64_t* epoch);
 
@@ -174,6 +191,12 @@ int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes);
  * itself (send/recv to self), which runs the RCCL path on a single GPU. */
 int gol_comm_unique_id(uint8_t id_out[GOL_UNIQUE_ID_BYTES]);
 int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank, int nranks);
+
+/* Tear down the context's communicator (ncclCommAbort: safe with a dead
+ * peer); gol_comm_init may then join a new ring.  The shard keeps its board
+ * and epoch.  Used when a lost backend is re-spawned and the survivors rebuild
+ * the ring around it (gameoflife/elastic.py). */
+int gol_comm_abort(gol_ctx* ctx);
 
 /* Sum-reduce `count` uint64 values (mod 2^64) across the communicator in
  * place (the per-generation hash reduction). */

@@ -1,7 +1,8 @@
 """CPU test double of gameoflife.elastic.GpuShard (torus, any rule mask):
 the shard steps with the oracle, halo rows and the hash reduction go over
-gloo.  Lets the CPU suite run the elastic supervisor/worker processes
-end to end.  Test infrastructure only (imports oracle/)."""
+gloo, and the light-cone replay of a lost block is the oracle stepping the
+block plus its light cone.  Lets the CPU suite run the elastic supervisor /
+worker processes end to end.  Test infrastructure only (imports oracle/)."""
 import os
 import sys
 
@@ -17,17 +18,26 @@ from oracle import oracle as O  # noqa: E402
 
 
 class OracleShard:
-    def __init__(self, width, height, row0, rows, rank, world, attempt_dir, topology="torus", rule="life"):
+    def __init__(self, width, height, row0, rows, topology="torus", rule="life", device=0):
         assert topology == "torus"
         self.W, self.H, self.row0, self.rows = width, height, row0, rows
         r = rule_by_name(rule)
         self.rule = (r.birth, r.survive)
-        self.world, self.epoch = world, 0
-        self.plan = HaloPlan(rank, world, True)
+        self.world, self.epoch = 1, 0
+        self.plan = HaloPlan(0, 1, True)
         self.board = None
+
+    def join(self, ring_dir, rank, world):
+        self.world = world
+        self.plan = HaloPlan(rank, world, True)
         if world > 1:
-            dist.init_process_group("gloo", init_method="file://" + os.path.join(attempt_dir, "gloo_store"),
+            dist.init_process_group("gloo", init_method="file://" + os.path.join(ring_dir, "gloo_store"),
                                     rank=rank, world_size=world)
+
+    def leave(self):
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        self.world = 1
 
     def seed(self, seed):
         self.board = O.seed_packed(self.W, self.H, seed, row0=self.row0, rows=self.rows)
@@ -58,20 +68,31 @@ class OracleShard:
         return recv["top"].numpy().view(np.uint32), recv["bot"].numpy().view(np.uint32)
 
     def step(self, n):
-        out = []
+        glob, part = [], []
         for _ in range(n):
             top, bot = self._halos()
             ext = np.vstack([top[None], self.board, bot[None]])
             self.board = O.step_packed(ext, self.W, O.TORUS, self.rule)[1:-1]
             self.epoch += 1
-            part = O.hash_packed(self.board, self.W, row0=self.row0)
+            p = O.hash_packed(self.board, self.W, row0=self.row0)
+            part.append(p)
             if self.world > 1:
-                t = torch.tensor([part - (1 << 64) if part >= (1 << 63) else part], dtype=torch.int64)
+                t = torch.tensor([p - (1 << 64) if p >= (1 << 63) else p], dtype=torch.int64)
                 dist.all_reduce(t)  # int64 sum wraps like uint64
-                part = int(t.item()) & ((1 << 64) - 1)
-            out.append(part)
-        return np.array(out, dtype=np.uint64)
+                p = int(t.item()) & ((1 << 64) - 1)
+            glob.append(p)
+        return np.array(glob, dtype=np.uint64), np.array(part, dtype=np.uint64)
 
     def close(self):
-        if self.world > 1:
-            dist.destroy_process_group()
+        self.leave()
+
+    @staticmethod
+    def replay_block(width, height, blob, above, below, depth, topology="torus", rule="life", device=0):
+        r = rule_by_name(rule)
+        h, data = parse_checkpoint(blob)
+        ext = np.vstack([above, data, below]).astype(np.uint32)
+        hs = []
+        for _ in range(depth):
+            ext = O.step_packed(ext, width, O.TORUS, (r.birth, r.survive))
+            hs.append(O.hash_packed(ext[depth:depth + h["rows"]], width, row0=h["row0"]))
+        return ext[depth:depth + h["rows"]].copy(), np.array(hs, dtype=np.uint64)

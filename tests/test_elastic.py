@@ -1,17 +1,22 @@
 """Cross-process fault path (gameoflife.elastic, BASELINE.json config 5):
-checkpoint files, re-sharded restore, and the supervisor killing a backend
-process mid-run and re-deploying the board on the survivors.  The CPU tests
-run real backend processes with the oracle/gloo shard double
-(tests/elastic_oracle_shard.py); the GPU test runs libgol backends."""
+checkpoint files, light-cone rows, and the supervisor crashing backend
+processes mid-run -- once, and recurrently on the reference's errors.delay /
+errors.every / max-crashes schedule -- with lost-shard-only recovery (the
+block is re-spawned next to a survivor and replayed alone; nobody rolls
+back).  The CPU tests run real backend processes with the oracle/gloo shard
+double (tests/elastic_oracle_shard.py); the GPU tests run libgol backends."""
 import os
 
+import numpy as np
 import pytest
 
 from gameoflife import elastic as E
+from gameoflife.board import SimulationParams, crash_schedule
 from oracle import oracle as O
 
 TESTS = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(TESTS)
+ORACLE_SHARD = "elastic_oracle_shard:OracleShard"
 
 
 def _env():
@@ -41,6 +46,46 @@ def test_checkpoint_roundtrip_and_reshard(tmp_path):
     # an epoch missing a shard is not complete
     E.write_shard_checkpoint(str(tmp_path), _blob(W, H, 0, 8, 50, board))
     assert E.complete_epochs(str(tmp_path), H) == [40]
+    assert E.covering_epochs(str(tmp_path), 0, 8) == [40, 50]
+    # overlapping blocks of two decompositions at one epoch (a merged block
+    # next to the blocks it replaced) hold the same rows: still complete
+    E.write_shard_checkpoint(str(tmp_path), _blob(W, H, 0, 16, 40, board))
+    assert E.complete_epochs(str(tmp_path), H) == [40]
+    assert (E.parse_checkpoint(E.assemble_checkpoint(str(tmp_path), 40, 3, 20))[1] == board[3:23]).all()
+
+
+def test_light_cone_rows(tmp_path):
+    W, H = 32 * 3, 20
+    board = O.seed_packed(W, H, 8)
+    for r0, n in [(0, 7), (7, 7), (14, 6)]:
+        E.write_shard_checkpoint(str(tmp_path), _blob(W, H, r0, n, 10, board))
+    up, dn = E.light_cone(str(tmp_path), 10, 7, 7, 3, H, torus=True)
+    assert (up == board[4:7]).all() and (dn == board[14:17]).all()
+    up, dn = E.light_cone(str(tmp_path), 10, 0, 7, 9, H, torus=True)  # wraps, deeper than a shard
+    assert (up == board[[11, 12, 13, 14, 15, 16, 17, 18, 19]]).all() and (dn == board[7:16]).all()
+    up, dn = E.light_cone(str(tmp_path), 10, 14, 6, 4, H, torus=False)  # clipped: dead beyond the edge
+    assert (up == board[10:14]).all() and (dn == 0).all()
+    # a block stepped with its light cone (torus in x, garbage ends) matches
+    # the whole board stepped the same number of generations
+    d = 5
+    up, dn = E.light_cone(str(tmp_path), 10, 7, 7, d, H, torus=True)
+    ext = np.vstack([up, board[7:14], dn])
+    for _ in range(d):
+        ext = O.step_packed(ext, W)
+    ref, _ = O.run_packed(board, W, d, want_hashes=False)
+    assert (ext[d:d + 7] == ref[7:14]).all()
+
+
+def test_crash_schedule_follows_reference_keys():
+    """BoardCreator.scala:97-108 timing: ticks at start + k * tick advance to
+    epoch k + 1; crash i at delay + i * every, at most max-crashes."""
+    p = SimulationParams(start_delay_ms=1000, tick_ms=3000, first_error_after_ms=10000, error_every_ms=15000,
+                         max_number_of_crashes=100)
+    assert [g for g, _ in crash_schedule(p, 30)] == [4, 9, 14, 19, 24, 29]
+    p2 = SimulationParams(start_delay_ms=0, tick_ms=1000, first_error_after_ms=7000, error_every_ms=9000,
+                          max_number_of_crashes=2)
+    assert [g for g, _ in crash_schedule(p2, 100)] == [8, 17]
+    assert crash_schedule(p2, 100, seed=5) == crash_schedule(p2, 100, seed=5)
 
 
 def _expected(W, H, gens, seed=0x5EED):
@@ -49,27 +94,50 @@ def _expected(W, H, gens, seed=0x5EED):
 
 
 @pytest.mark.parametrize("world,kill", [(3, (1, 25)), (2, (0, 17))])
-def test_kill_backend_process_and_redeploy(tmp_path, world, kill):
+def test_kill_backend_process_and_respawn_alone(tmp_path, world, kill):
     W, H, gens = 32 * 8, 60, 50
-    sup = E.Supervisor(W, H, gens, world, str(tmp_path), ckpt_every=10, shard="elastic_oracle_shard:OracleShard",
+    sup = E.Supervisor(W, H, gens, world, str(tmp_path), ckpt_every=10, shard=ORACLE_SHARD,
                        kill=kill, timeout=240, env=_env())
     got = sup.run()
     kinds = [e["event"] for e in sup.events]
-    assert kinds == ["deploy", "inject-crash", "lost", "deploy"], sup.events
+    assert kinds == ["deploy", "inject-crash", "lost"], sup.events
     lost = sup.events[2]
-    assert kill[0] in lost["ranks"] and lost["new_world"] == world - len(lost["ranks"])
-    # restarted from the last complete checkpoint before the crash
-    assert lost["restart_epoch"] == kill[1] // 10 * 10
+    # only the lost block replays, from its last checkpoint; the others stay
+    assert lost["checkpoint_epoch"] == kill[1] // 10 * 10 and lost["epoch"] == kill[1]
+    assert lost["replayed_generations"] == kill[1] % 10 and lost["new_world"] == world - 1
+    assert "absorbed_by" in lost
+    assert got == _expected(W, H, gens)
+
+
+def test_recurring_crashes_on_the_reference_schedule(tmp_path):
+    """errors.delay / errors.every / max-crashes drive repeated crashes: 3
+    backends shrink to 1, then the last one dies twice and is re-spawned from
+    the checkpoint files alone; every generation's hash equals the
+    uninterrupted oracle run."""
+    W, H, gens = 32 * 6, 45, 48
+    p = SimulationParams(start_delay_ms=0, tick_ms=1000, first_error_after_ms=6000, error_every_ms=11000,
+                         max_number_of_crashes=4)
+    crashes = crash_schedule(p, gens, seed=3)
+    assert [g for g, _ in crashes] == [7, 18, 29, 40]
+    sup = E.Supervisor(W, H, gens, 3, str(tmp_path), ckpt_every=5, shard=ORACLE_SHARD, crashes=crashes,
+                       chunk=3, timeout=400, env=_env())
+    got = sup.run()
+    lost = [e for e in sup.events if e["event"] == "lost"]
+    assert len(lost) == 4
+    assert [e["new_world"] for e in lost] == [2, 1, 1, 1]
+    assert "respawned_as" in lost[2] and "respawned_as" in lost[3]
     assert got == _expected(W, H, gens)
 
 
 @pytest.mark.gpu
 def test_kill_gpu_backend_and_respawn(gpu, tmp_path):
-    """One GPU: the lost backend's board is re-spawned on the surviving GPU
-    (the same one here) from the last checkpoint and replayed."""
+    """One GPU, one backend crashed three times: each time a fresh backend
+    restores the board from the checkpoint files and replays the lost
+    generations alone (gol_replay on the whole torus: the light cone wraps)."""
     W, H, gens = 32 * 300, 120, 50
-    sup = E.Supervisor(W, H, gens, 1, str(tmp_path), ckpt_every=10, kill=(0, 25), timeout=240, env=_env())
+    sup = E.Supervisor(W, H, gens, 1, str(tmp_path), ckpt_every=10, crashes=[(13, 0), (25, 0), (40, 0)],
+                       chunk=4, timeout=400, env=_env())
     got = sup.run()
-    assert [e["event"] for e in sup.events] == ["deploy", "inject-crash", "lost", "deploy"], sup.events
-    assert sup.events[2]["restart_epoch"] == 20
+    lost = [e for e in sup.events if e["event"] == "lost"]
+    assert [(e["checkpoint_epoch"], e["epoch"]) for e in lost] == [(10, 13), (20, 25), (30, 40)]
     assert got == _expected(W, H, gens)

@@ -75,12 +75,13 @@ def test_group_rejects_bad_layout_and_lost_shard(gpu):
     a.close()
 
 
-@pytest.mark.parametrize("ckpt_dir", [False, True])
-def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir):
+@pytest.mark.parametrize("ckpt_dir,mode", [(False, "light-cone"), (True, "light-cone"), (False, "rollback")])
+def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir, mode):
     """BASELINE.json config 5 in miniature: 8 shards, checkpoint every 10,
-    shard 3 killed at generation 25 of 50, re-spawned next to a survivor,
-    rolled back and replayed: every per-generation hash equals the
-    uninterrupted run's, and the final board equals the oracle's."""
+    shard 3 killed at generation 25 of 50 and re-spawned next to a survivor --
+    alone from its checkpoint and its neighbours' light cone (the others keep
+    their state), or by a global rollback: every per-generation hash equals
+    the uninterrupted run's, and the final board equals the oracle's."""
     from gameoflife import _native as N
     from gameoflife.fault import ShardedSimulation
     W, H = 32 * 256, 1024
@@ -96,8 +97,15 @@ def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir):
     sim.kill(3)
     with pytest.raises(RuntimeError):
         sim.step(1)
-    replayed = sim.respawn(3)
+    replayed = sim.respawn(3, mode=mode)
     assert len(replayed) == 5 and sim.epoch == 25
+    if mode == "light-cone":  # shard 3's own partial hashes of generations 21..25
+        row0, rows = N.shard_rows(H, 3, 8)
+        b = O.seed_packed(W, H, 0x5EED)
+        b, _ = O.run_packed(b, W, 20, want_hashes=False)
+        for g in range(5):
+            b, _ = O.run_packed(b, W, 1, want_hashes=False)
+            assert replayed[g] == O.hash_packed(b[row0:row0 + rows], W, row0=row0), g
     got += sim.step(25)
     assert got == want
     assert sim.hashes == want
@@ -109,3 +117,29 @@ def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir):
     final, oh = O.run_packed(board0, W, 50, O.TORUS, O.LIFE)
     assert [int(x) for x in oh] == want
     assert (final == ref_board).all()
+
+
+@pytest.mark.parametrize("topology", ["torus", "ref-clipped"])
+def test_recurring_crashes_light_cone(gpu, topology):
+    """Crashes on the reference's schedule (errors.delay / errors.every /
+    max-crashes, board.crash_schedule): each lost shard is re-spawned alone
+    from its checkpoint and its neighbours' light cone -- including light
+    cones deeper than a neighbour shard (checkpoint every 12, shards of 9-10
+    rows) -- and the hashes equal the uninterrupted oracle run."""
+    from gameoflife import _native as N
+    from gameoflife.board import SimulationParams, crash_schedule
+    from gameoflife.fault import ShardedSimulation
+    W, H, gens = 32 * 100 + (0 if topology == "torus" else 13), 77, 60
+    p = SimulationParams(start_delay_ms=0, tick_ms=100, first_error_after_ms=500, error_every_ms=1100,
+                         max_number_of_crashes=5)
+    crashes = crash_schedule(p, gens, seed=11)
+    assert len(crashes) == 5
+    sim = ShardedSimulation(W, H, 8, list(range(N.device_count())), topology=topology, checkpoint_every=12)
+    got = sim.run(gens, crashes)
+    board = sim.snapshot()
+    assert sum(e.startswith("respawn") for e in sim.events) == 5
+    sim.close()
+    topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
+    final, want = O.run_packed(O.seed_packed(W, H, 0x5EED), W, gens, topo, O.LIFE)
+    assert got == [int(x) for x in want]
+    assert (board == final).all()

@@ -342,3 +342,28 @@ def test_step_ex_checks_hash_capacity(gpu):
         assert e.epoch == 4 and buf[-1] == e.hash()
         assert N.lib.gol_step_ex(e._h, 3, ctypes.cast(None, N._u64p), 0) == N.GOL_OK
         assert e.epoch == 7
+
+
+@pytest.mark.parametrize("W,topology", [(32 * 70, "torus"), (32 * 71, "torus"), (32 * 40 + 5, "ref-clipped")])
+@pytest.mark.parametrize("row0,rows,d", [(10, 9, 4), (0, 12, 7), (30, 10, 13), (0, 40, 3)])
+def test_replay_light_cone(gpu, W, topology, row0, rows, d):
+    """gol_replay: a shard restored at epoch e, given the d rows above and
+    below it at epoch e (wrapping on a torus, dead beyond a clipped edge),
+    advances d generations alone exactly as the whole board does; its
+    per-generation partial hashes are the whole board's rows' hashes."""
+    from gameoflife.elastic import light_cone_from
+    H = 40
+    topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
+    board = O.seed_packed(W, H, row0 * 7 + d)
+    with engine(W, H, topology=topology, rule=rule_obj(O.LIFE), row0=row0, rows=rows) as e:
+        e.load(board[row0:row0 + rows])
+        up, dn = light_cone_from(lambda idx: board[idx], row0, rows, d, H, topology == "torus", e.wwords)
+        got = e.replay(d, up, dn)
+        assert e.epoch == d
+        cur = board
+        for g in range(d):
+            cur, _ = O.run_packed(cur, W, 1, topo, O.LIFE, want_hashes=False)
+            assert got[g] == O.hash_packed(cur[row0:row0 + rows], W, row0=row0, topology=topo), g
+        assert (e.snapshot() == cur[row0:row0 + rows]).all()
+        with pytest.raises(Exception):
+            e.replay(2, up[:1], dn[:1])  # light-cone rows of the wrong depth
