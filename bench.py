@@ -102,8 +102,11 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
     eng.step(steps, hashes=with_hash)
     eng.sync()
     torch.cuda.synchronize()
-    barrier(dist, world)
+    # the clock stops when this rank's work is done; the closing barrier and
+    # the max over ranks then give the job's time (a gloo barrier costs
+    # ~1 ms, a real share of an N = 8 rank's 20-step window)
     dt = time.perf_counter() - t0
+    barrier(dist, world)
     kms, launches, gens = eng.profile_read()
     eng.profile(False)
     if world > 1:
@@ -279,23 +282,27 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     ncclSend/ncclRecv to itself, then the boundary rows on the edge stream).
     (1) the whole board, (2) one rank's shard of the N = 8 decomposition
     (262144 x 32768): what each of 8 ranks computes, without the xGMI latency
-    of a real ring."""
+    of a real ring.  Both with >= 48 warm-up generations: after the GPU idles
+    (here: the shard's allocation) the first ~20 launches run 10-25 % slower
+    while the power management settles (profiles/r02_warmup_curve.txt), which
+    a 6-generation warm-up of a 0.08 ms-per-generation shard does not cover."""
     out = {}
+    warm = max(a.warmup, 48)
     eng.comm_init(N.unique_id(), 0, 1)
     eng.seed(0x5EED)
-    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
+    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, warm, False)
     out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
-                                    "ms_per_step": round(dt / a.steps * 1e3, 4),
+                                    "warmup": warm, "ms_per_step": round(dt / a.steps * 1e3, 4),
                                     "pass_plan": eng.pass_plan(min(a.steps, 1024))}
     rows8 = H // 8
     with GolEngine(W, H, topology="torus", rule="life", device=local, row0=0, rows=rows8) as e8:
         e8.comm_init(N.unique_id(), 0, 1)  # a 1-rank ring over a shard-sized torus
         e8.seed(0x5EED)
-        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, warm, False)
         plan8 = e8.pass_plan(min(a.steps, 1024))
     out["per_rank_shard_self_ring"] = {
         "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
-        "unit": "GCUPS", "ms_per_step": round(dt8 / a.steps * 1e3, 4), "pass_plan": plan8,
+        "unit": "GCUPS", "warmup": warm, "ms_per_step": round(dt8 / a.steps * 1e3, 4), "pass_plan": plan8,
         "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
                                     f"{W}x{rows8}", "ring")}
     return out
