@@ -271,6 +271,12 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
     // band 216 1.5-10 % faster on two boxes; with more rounds the effect is
     // within box-to-box noise (profiles/r01_band_quantization.txt).  Narrow
     // boards (< 32 strips) keep the plain choice (the model mispredicts 65536^2).
+    // Narrow boards at 7- and 8-generation passes (4 waves per SIMD): 256-row
+    // bands with the tail split below.  Same-box sweep at 65536^2, G = 8
+    // (profiles/r02_band_sweep.txt): 0.0384 ms per generation vs 0.0405 for
+    // the plain choice (137 rows, no tail) and 0.0471 for 256 rows without
+    // the tail; at G = 6 the plain choice stays best.
+    if (strips < 32 && gens >= 7 && resident > 0) return (int)std::min<int64_t>(256, std::max<int64_t>(rows, 1));
     if (resident > 0 && strips >= 32) {
         auto cost = [&](int64_t b) -> double {
             const int64_t waves = (rows + b - 1) / b * strips;
@@ -312,7 +318,7 @@ struct TailSplit {
 constexpr double kTailFrac = 1.0;
 constexpr int kTailDiv = 3;
 
-TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int64_t resident) {
+TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int64_t resident, int gens) {
     double frac = kTailFrac;
     int div = kTailDiv;
     const char* env = getenv("GOL_TAIL");
@@ -323,8 +329,9 @@ TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int
     }
     TailSplit t;
     // narrow boards (< 32 strips, e.g. 65536^2 with 17) measured neutral to
-    // -3.6 % (profiles/r01_tail_sweep.txt, r01_band_sweep.txt): off unless forced
-    if (frac <= 0.0 || div < 2 || resident <= 0 || strips <= 0 || (!env && strips < 32)) return t;
+    // -3.6 % at G = 6 (profiles/r01_tail_sweep.txt, r01_band_sweep.txt): off
+    // unless forced; at G >= 7 they take 256-row bands (pick_band), which need it
+    if (frac <= 0.0 || div < 2 || resident <= 0 || strips <= 0 || (!env && strips < 32 && gens < 7)) return t;
     const int64_t waves = (rows + band - 1) / band * strips;
     if (waves <= resident) return t;  // a single round: nothing to even out
     const int b2 = std::max(8, band / div);
@@ -396,7 +403,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         rhi[k] = hi[k];
     }
     if (n == 1 && gens > 1) {
-        const TailSplit t = tail_split(ctx, hi[0] - lo[0], p.strips, band, resident);
+        const TailSplit t = tail_split(ctx, hi[0] - lo[0], p.strips, band, resident, gens);
         if (t.rows > 0) {  // bulk [lo, hi - t.rows) in `band` rows, tail in t.band rows
             nr = 2;
             rhi[0] = hi[0] - t.rows;

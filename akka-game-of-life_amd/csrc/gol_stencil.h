@@ -393,6 +393,9 @@ __device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool
 // The horizontal-first kernel keeps its per-generation sums in LDS, one u64
 // per lane, pair and generation, added to with ds_add_u64 (no return): 2G
 // fewer VGPRs than register sums, which at G = 6..8 is a wave per SIMD.
+#ifndef GOL_HASH_LDS
+#define GOL_HASH_LDS 1
+#endif
 template <int VEC>
 __device__ __forceinline__ void hash_row_lds(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
                                              unsigned long long* slot) {
@@ -837,6 +840,9 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 #pragma unroll
             for (int k = 0; k < G * kNP; ++k) hsum[k * kWaveLanes] = 0ull;
         }
+        HashAcc<VEC> hreg[GOL_HASH_LDS ? 1 : G];  // -DGOL_HASH_LDS=0: register sums (A/B builds)
+#pragma unroll
+        for (int s = 0; s < (GOL_HASH_LDS ? 1 : G); ++s) hash_clear(hreg[s]);
         const bool up = (bandi & 1) != 0;
         auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
         auto vis = [&](int m) -> bool { return row_visible<CLIPPED>(p, brow(m)); };
@@ -897,7 +903,13 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
                                             hr[s - 1][((u - s) % 3 + 3) % 3],
                                             hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
                 const bool own_row = m >= G && m < n_in - G;
-                if constexpr (HASH) hash_row_lds<VEC>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
+                if constexpr (HASH) {
+#if GOL_HASH_LDS
+                    hash_row_lds<VEC>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
+#else
+                    hash_row_keys<VEC>(kae[s], kao[s], o, odd_lane, hreg[s - 1]);
+#endif
+                }
                 if (s < G) {
                     arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
                 } else {
@@ -928,7 +940,10 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
             for (int s = 0; s < G; ++s) {
                 HashAcc<VEC> h;
 #pragma unroll
-                for (int k = 0; k < kNP; ++k) h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
+                for (int k = 0; k < kNP; ++k) {
+                    if constexpr (GOL_HASH_LDS) h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
+                    else h.a[k] = hreg[s].a[k];
+                }
                 acc[s] = hash_lane_total(h, col, owns);
             }
         }
