@@ -41,7 +41,8 @@ def main():
     tot = lambda f: sum(v for k, v in cnt.items() if f(k))
     print(name)
     print("VALU", tot(lambda k: k.startswith("v_")), "SALU", tot(lambda k: k.startswith("s_")),
-          "branches", tot(lambda k: "branch" in k), "loads", tot(lambda k: "load" in k))
+          "branches", tot(lambda k: "branch" in k), "loads", tot(lambda k: "load" in k),
+          "scratch", tot(lambda k: k.startswith("scratch_")))
     for k, v in cnt.most_common(int(sys.argv[3]) if len(sys.argv) > 3 else 14):
         print(f"{v:6d} {k}")
 
