@@ -21,7 +21,6 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = ("step_kernel", "multistep_kernel", "multistep_hg_kernel")
-GENS = {262144: 60, 65536: 102}  # timed generations of bench.py's two boards
 
 
 def rows(path):
@@ -59,16 +58,43 @@ def main():
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         groups[(r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]))].append(dur)
     b = benches["bench_under_rocprof.json"]
-    lines = ["rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 60 --warmup 6",
+    lines = [f"rocprofv3 --kernel-trace --stats -- python3 bench.py --steps {b['steps']} --warmup {b['warmup']}",
              "per (kernel, grid): dispatches, mean / median / min ms", ""]
     for (name, gx, gy), d in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"{name:40s} grid=({gx},{gy}) n={len(d):3d} mean={statistics.mean(d):.4f} "
                      f"median={statistics.median(d):.4f} min={min(d):.4f}")
-    lines += ["", "bench.py HIP-event numbers from the same run (timed region only):",
-              f"  main workload   avg_launch_ms={b['roofline']['avg_launch_ms']} launches={b['roofline']['launches']}",
-              f"  secondary       avg_launch_ms={b['secondary']['roofline']['avg_launch_ms']} "
-              f"launches={b['secondary']['roofline']['launches']}",
-              "(rocprof's counts include the warm-up launch of each workload)"]
+    lines += ["", "bench.py HIP-event numbers from the same run (timed region only) beside the trace:"]
+
+    def instance(G, hashed):
+        # multistep_hg_kernel<2, G, LIFE, HASH, torus, pairs> (step_kernel<2, ...> at G = 1)
+        h = "true" if hashed else "false"
+        if G == 1:
+            return f"step_kernel<2, true, {h}, false, true>"
+        return f"multistep_hg_kernel<2, {G}, true, {h}, false, true>"
+
+    def traced(plan, hashed):
+        # the plan's launches at the largest grid of each instance: the
+        # whole-board launches (warm-up launches of the same depth included)
+        tot, n = 0.0, 0
+        for G in plan:
+            cands = [(gx, d) for (name, gx, gy), d in groups.items() if instance(G, hashed) in name]
+            if not cands:
+                return None
+            gx, d = max(cands)
+            tot += statistics.mean(d)
+            n += 1
+        return tot / n
+
+    for label, rec, hashed in (("main workload", b, False), ("with_state_hash", b.get("with_state_hash"), True)):
+        if not rec or not rec.get("roofline"):
+            continue
+        ro = rec["roofline"]
+        plan = rec.get("pass_plan") or ro.get("pass_plan") or b.get("pass_plan")
+        t = traced(plan, hashed) if plan else None
+        lines.append(f"  {label:16s} bench avg_launch_ms={ro.get('avg_launch_ms')} launches={ro.get('launches')}"
+                     + (f"   rocprof plan-weighted mean={t:.4f} ms" if t else ""))
+    lines.append("(rocprof's per-instance means also hold the warm-up launches and the N = 1 ring-schedule runs'")
+    lines.append(" launches of the same instance and grid; the bench's numbers are its timed launches only)")
     with open(os.path.join(dst, f"{tag}_kernel_trace.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
