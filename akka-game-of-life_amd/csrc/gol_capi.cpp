@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -598,8 +599,18 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
 // same depths (their halo messages must match), so a sharded pass is capped
 // by the smallest shard of the decomposition, floor(H / N) (a 1-rank ring
 // sends G of its own rows: G <= H).
+// Planned (not fixed) passes deeper than kMaxGensPlannedGeneric run only on
+// the B3/S23 torus kernels: the generic-rule and clipped instances hold their
+// rule masks / visibility planes in registers and drop to 2 waves per SIMD at
+// G >= 10 (scripts/resource_usage.py), and the cost table is measured on the
+// B3/S23 torus.
+constexpr int kMaxGensPlannedGeneric = 8;
+
 int depth_cap(const gol_ctx* ctx) {
-    int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass : gol::kMaxGensPerPass;
+    const bool life_torus = ctx->topology == GOL_TORUS && ctx->birth == GOL_RULE_LIFE_BIRTH &&
+                            ctx->survive == GOL_RULE_LIFE_SURVIVE;
+    int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass
+                                       : (life_torus ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
     if (ctx->nccl) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
@@ -607,26 +618,31 @@ int depth_cap(const gol_ctx* ctx) {
 }
 
 // Pass planner (DESIGN.md section 4 "Pass planner").  Relative time of one
-// pass of G generations (G = 1..8, G = 6 -> 1) on the multi-generation
+// pass of G generations (G = 1..12, G = 6 -> 1) on the multi-generation
 // kernels, from scripts/depth_sweep.py (profiles/r01_depth_sweep.txt, two
 // boxes): up to G = 6 a pass costs about the same (the sweep over the plane
-// is HBM-bound), G = 7 and 8 cost more but less per generation on wide boards
-// (>= 32 column strips); narrow boards are best at 6.
+// is HBM-bound), deeper passes cost more but less per generation on wide
+// boards (>= 32 column strips); narrow boards are best at 8.
+// G = 9..12 (round 2, 3 waves/SIMD at G >= 10): fresh-board depth sweep
+// (profiles/r02_depth_sweep_deep.txt) calibrated by same-box pass mixes
+// (profiles/r02_plan_mix_ab.txt: 20 generations 12 + 8 at 111.1k GCUPS vs
+// 6 + 6 + 8 at 103.6k; 60 generations 5 x 12 at 119.0k vs 6 x 10 at 115.0k).
 // With the fused per-generation hash the kernels are VALU-bound from G = 6
-// on; per generation 6 is best, 7 close behind on wide boards (HASH=1 rows,
-// profiles/r02_depth_sweep_hash.txt: the one-multiply-add hash with LDS sums).
+// on; per generation 6 and 10 are best on wide boards, 6 on narrow ones
+// (HASH=1 rows; G >= 11 hashed drops to 2-3 waves/SIMD).
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
-    // [hashed][wide]
-    {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26},       // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
-     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231}},       // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
-    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.262, 1.475},     // narrow, hashed (65536^2)
-     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.186, 1.395}}};  // wide, hashed (262144^2)
+    // [hashed][wide]; G = 0 .. 12
+    {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26, 1.457, 1.657, 1.829, 1.995},    // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
+     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231, 1.37, 1.52, 1.70, 1.77}},        // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
+    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.262, 1.475, 1.627, 1.788, 2.365, 2.547},  // narrow, hashed (65536^2)
+     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.186, 1.395, 1.516, 1.645, 2.20, 2.30}}};  // wide, hashed (262144^2)
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);
 // otherwise the plan minimises the summed pass cost (a DP over n, n <= 1024:
-// callers plan per chunk).  Deterministic in (width, height, N, n), so all
-// shards of a ring plan alike.
+// callers plan per chunk), deepest passes first (12 + 8 ran 3 % faster than
+// 8 + 12 from the bench's fresh board, profiles/r02_plan_mix_ab.txt).
+// Deterministic in (width, height, N, n), so all shards of a ring plan alike.
 std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n, bool hashed) {
     const int cap = depth_cap(ctx);
     std::vector<int> plan;
@@ -650,6 +666,7 @@ std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n, bool hashed) {
         }
     }
     for (uint32_t k = n; k > 0; k -= (uint32_t)pick[k]) plan.push_back(pick[k]);
+    std::sort(plan.begin(), plan.end(), std::greater<int>());
     return plan;
 }
 

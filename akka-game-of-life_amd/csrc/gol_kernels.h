@@ -11,7 +11,7 @@ constexpr int kWavesPerWG = 4;   // 256-thread workgroups
 constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line each)
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
-constexpr int kMaxGensPerPass = 8;  // temporal blocking depth supported by the kernels
+constexpr int kMaxGensPerPass = 12;  // temporal blocking depth supported by the kernels
 
 // State hash keys (DESIGN.md "State hash"; oracle/gol_oracle.c
 // oracle_hash_packed, oracle/oracle.py np_hash): device word w at global row

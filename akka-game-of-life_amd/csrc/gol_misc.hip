@@ -126,6 +126,10 @@ hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool h
         case 6: return launch_step_g6(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
         case 7: return launch_step_g7(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
         case 8: return launch_step_g8(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 9: return launch_step_g9(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 10: return launch_step_g10(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 11: return launch_step_g11(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
+        case 12: return launch_step_g12(p, vec, life, hash, clipped, pairs, grid_x, grid_y, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -140,6 +144,10 @@ int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash,
         case 6: return blocks_step_g6(vec, variant, life, hash, clipped, pairs);
         case 7: return blocks_step_g7(vec, variant, life, hash, clipped, pairs);
         case 8: return blocks_step_g8(vec, variant, life, hash, clipped, pairs);
+        case 9: return blocks_step_g9(vec, variant, life, hash, clipped, pairs);
+        case 10: return blocks_step_g10(vec, variant, life, hash, clipped, pairs);
+        case 11: return blocks_step_g11(vec, variant, life, hash, clipped, pairs);
+        case 12: return blocks_step_g12(vec, variant, life, hash, clipped, pairs);
         default: return 0;
     }
 }

@@ -1068,6 +1068,10 @@ hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, bool, int, i
 hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
 hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g9(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g10(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g11(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
+hipError_t launch_step_g12(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
 int blocks_step_g1(int, int, bool, bool, bool, bool);
 int blocks_step_g2(int, int, bool, bool, bool, bool);
 int blocks_step_g3(int, int, bool, bool, bool, bool);
@@ -1076,5 +1080,9 @@ int blocks_step_g5(int, int, bool, bool, bool, bool);
 int blocks_step_g6(int, int, bool, bool, bool, bool);
 int blocks_step_g7(int, int, bool, bool, bool, bool);
 int blocks_step_g8(int, int, bool, bool, bool, bool);
+int blocks_step_g9(int, int, bool, bool, bool, bool);
+int blocks_step_g10(int, int, bool, bool, bool, bool);
+int blocks_step_g11(int, int, bool, bool, bool, bool);
+int blocks_step_g12(int, int, bool, bool, bool, bool);
 
 }  // namespace gol

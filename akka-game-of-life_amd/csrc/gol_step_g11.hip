@@ -1,0 +1,16 @@
+// gol_step_g11.hip -- instantiates the 11-generation-per-pass step kernels
+// (one translation unit per pass depth so they compile in parallel).
+#include "gol_stencil.h"
+
+namespace gol {
+
+hipError_t launch_step_g11(const StepParams& p, int vec, bool life, bool hash, bool clipped, bool pairs, int gx,
+                          int gy, hipStream_t st) {
+    return dev::launch_gens<11>(p, vec, life, hash, clipped, pairs, gx, gy, st);
+}
+
+int blocks_step_g11(int vec, int variant, bool life, bool hash, bool clipped, bool pairs) {
+    return dev::blocks_gens<11>(vec, variant, life, hash, clipped, pairs);
+}
+
+}  // namespace gol

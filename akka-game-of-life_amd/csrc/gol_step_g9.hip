@@ -1,0 +1,16 @@
+// gol_step_g9.hip -- instantiates the 9-generation-per-pass step kernels
+// (one translation unit per pass depth so they compile in parallel).
+#include "gol_stencil.h"
+
+namespace gol {
+
+hipError_t launch_step_g9(const StepParams& p, int vec, bool life, bool hash, bool clipped, bool pairs, int gx,
+                          int gy, hipStream_t st) {
+    return dev::launch_gens<9>(p, vec, life, hash, clipped, pairs, gx, gy, st);
+}
+
+int blocks_step_g9(int vec, int variant, bool life, bool hash, bool clipped, bool pairs) {
+    return dev::blocks_gens<9>(vec, variant, life, hash, clipped, pairs);
+}
+
+}  // namespace gol

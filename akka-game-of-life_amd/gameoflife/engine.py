@@ -177,7 +177,7 @@ class GolEngine:
 
     def set_tuning(self, band_rows: int = 0, gens_per_pass: int = 0, words_per_lane: int = 0) -> None:
         """Performance knobs only (gol_set_tuning): rows per band, generations
-        per HBM pass (1..8), words per lane (1/2/4, 0 = auto)."""
+        per HBM pass (1..12), words per lane (1/2/4, 0 = auto)."""
         self._chk(N.lib.gol_set_tuning(self._h, band_rows, gens_per_pass, words_per_lane))
 
 

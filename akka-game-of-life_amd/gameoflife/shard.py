@@ -27,14 +27,16 @@ def shard_rows_py(height: int, rank: int, nranks: int) -> tuple[int, int]:
     return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
 
-MAX_GENS_PER_PASS = 8  # gol_kernels.h kMaxGensPerPass
+MAX_GENS_PER_PASS = 12  # gol_kernels.h kMaxGensPerPass
+MAX_GENS_PLANNED_GENERIC = 8  # gol_capi.cpp kMaxGensPlannedGeneric
 
 
-def ring_depth_cap(height: int, nranks: int, gens_per_pass: int = 0) -> int:
+def ring_depth_cap(height: int, nranks: int, gens_per_pass: int = 0, life_torus: bool = True) -> int:
     """Deepest pass a ring may run (gol_capi.cpp depth_cap): every rank must
     issue identical halo messages, so the depth is capped by the smallest
-    shard, floor(H / N) rows (a 1-rank self-ring: H)."""
-    g = gens_per_pass if gens_per_pass > 0 else MAX_GENS_PER_PASS
+    shard, floor(H / N) rows (a 1-rank self-ring: H).  Planned passes of
+    other rules / the clipped topology stop at 8."""
+    g = gens_per_pass if gens_per_pass > 0 else (MAX_GENS_PER_PASS if life_torus else MAX_GENS_PLANNED_GENERIC)
     return max(1, min(g, MAX_GENS_PER_PASS, height // nranks))
 
 

@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")
     ap.add_argument("--band", type=int, default=0, help="rows per band (0 = auto)")
     ap.add_argument("--gpp", type=int, default=DEFAULT_GPP,
-                    help="generations fused per HBM pass (temporal blocking depth 1..8; 0 = automatic)")
+                    help="generations fused per HBM pass (temporal blocking depth 1..12; 0 = automatic)")
     ap.add_argument("--hash", action="store_true", help="fuse the per-generation state hash")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-ring", action="store_true", help="skip the N = 1 ring-schedule measurements")
@@ -364,7 +364,7 @@ def main():
     eng.seed(0x5EED)
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
-    eng_info = {g: eng.occupancy(g) for g in range(1, 9)}
+    eng_info = {g: eng.occupancy(g) for g in range(1, 13)}
     plan = eng.pass_plan(min(a.steps, 1024), hashes=a.hash)
     value = W * H * a.steps / dt / 1e9
     hashed = None

@@ -230,7 +230,7 @@ int gol_profile_reset(gol_ctx* ctx);
 /* Tuning knobs (results never depend on them); 0 selects the automatic
  * choice, which is also the default of a new context:
  *   band_rows       rows of output streamed by one wave;
- *   gens_per_pass   generations fused per HBM pass (temporal blocking, 1..8;
+ *   gens_per_pass   generations fused per HBM pass (temporal blocking, 1..12;
  *                   automatic: the pass planner, see gol_pass_plan);
  *   words_per_lane  32-bit words each lane owns per row (1, 2 or 4; must
  *                   divide the words of a row). */

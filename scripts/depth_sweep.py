@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""Time of one pass at each temporal-blocking depth G = 1..8 (reseeded board,
+"""Time of one pass at each temporal-blocking depth G = 1..12 (reseeded board,
 6 warm-up generations, 24 timed generations, min of ROUNDS interleaved rounds):
 the cost table behind gol_step's pass planner.
 
-    python scripts/depth_sweep.py [WxH ...]     env: ROUNDS=3  HASH=1 (fused hashes)
+    python scripts/depth_sweep.py [WxH ...]     env: ROUNDS=3  HASH=1 (fused hashes)  MAXG=12
 """
 import os
 import sys
@@ -19,12 +19,14 @@ def main():
         [(262144, 262144), (262144, 32768), (65536, 65536)]
     rounds = int(os.environ.get("ROUNDS", "3"))
     hashes = os.environ.get("HASH", "0") == "1"
+    maxg = int(os.environ.get("MAXG", "12"))
     for W, H in shapes:
         with GolEngine(W, H) as e:
             res = {}
             for _ in range(rounds):
-                for G in range(1, 9):
+                for G in range(1, maxg + 1):
                     gens = 24 if 24 % G == 0 else G * (24 // G + 1)
+                    gens = max(gens, 2 * G)
                     e.set_tuning(gens_per_pass=G)
                     e.seed(0x5EED)
                     e.step(6)
@@ -36,7 +38,7 @@ def main():
                     e.profile(False)
                     res.setdefault(G, []).append(ms / n)
             base = min(res[6])
-            for G in range(1, 9):
+            for G in range(1, maxg + 1):
                 t = min(res[G])
                 print(f"shape={W}x{H} hash={int(hashes)} G={G} ms/pass={t:.4f} ms/gen={t / G:.4f} pass/pass(G=6)={t / base:.3f} "
                       f"GCUPS={W * H * G / t / 1e6:9.1f}", flush=True)

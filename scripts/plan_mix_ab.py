@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
-"""Same-box A/B of explicit pass mixes for 60 generations at 262144^2 (each
-segment run at a fixed gens_per_pass): the planner's 4 x 7 + 4 x 8 against
-2 x 6 + 6 x 8 and 7 x 8 + 4 (DESIGN.md "Pass planner").
+"""Same-box A/B of explicit pass mixes (each pass run at a fixed
+gens_per_pass) on the bench's fresh board: reseed, a 5-generation warm-up,
+then the timed passes; interleaved rounds (DESIGN.md "Pass planner").
 
-    python scripts/plan_mix_ab.py [ROUNDS]
+    python scripts/plan_mix_ab.py [--shape WxH] [--rounds R] [--hash] 6,6,8 10,10 8,12 ...
 """
+import argparse
 import os
 import sys
 import time
@@ -14,33 +15,41 @@ sys.path.insert(0, os.path.join(ROOT, "akka-game-of-life_amd"))
 
 from gameoflife.engine import GolEngine  # noqa: E402
 
-MIXES = {"4x7+4x8": [(7, 28), (8, 32)], "2x6+6x8": [(6, 12), (8, 48)], "7x8+4": [(8, 56), (4, 4)],
-         "10x6": [(6, 60)]}
 
-
-def run(e, mix):
+def run(e, plan, hashed):
     e.seed(0x5EED)
-    e.set_tuning(gens_per_pass=6)
-    e.step(6)
+    e.set_tuning(gens_per_pass=0)
+    e.step(5, hashes=hashed)
     e.sync()
     t0 = time.perf_counter()
-    for g, n in mix:
+    for g in plan:
         e.set_tuning(gens_per_pass=g)
-        e.step(n)
+        e.step(g, hashes=hashed)
     e.sync()
     return time.perf_counter() - t0
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    W = H = 262144
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="262144x262144")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--hash", action="store_true")
+    ap.add_argument("plans", nargs="+")
+    a = ap.parse_args()
+    W, H = (int(x) for x in a.shape.split("x"))
+    plans = {p: [int(g) for g in p.split(",")] for p in a.plans}
     with GolEngine(W, H) as e:
-        for mix in MIXES.values():  # load every depth once
-            run(e, mix)
-        for r in range(rounds):
-            for name, mix in MIXES.items():
-                dt = run(e, mix)
-                print(f"r{r + 1} {name:8s} {dt * 1e3:8.3f} ms  {W * H * 60 / dt / 1e9:9.1f} GCUPS", flush=True)
+        for plan in plans.values():  # load every depth once
+            run(e, plan, a.hash)
+        best = {}
+        for r in range(a.rounds):
+            for name, plan in plans.items():
+                dt = run(e, plan, a.hash)
+                gc = W * H * sum(plan) / dt / 1e9
+                best[name] = max(best.get(name, 0.0), gc)
+                print(f"{a.shape} hash={int(a.hash)} r{r + 1} {name:12s} {dt * 1e3:8.3f} ms  {gc:9.1f} GCUPS", flush=True)
+        for name, gc in best.items():
+            print(f"{a.shape} hash={int(a.hash)} best {name:12s} {gc:9.1f} GCUPS", flush=True)
 
 
 if __name__ == "__main__":

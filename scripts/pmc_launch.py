@@ -11,7 +11,8 @@ per step-kernel launch of each (shape, mode, pass depth G, hash) --
 
 Launches: the step-kernel dispatches with the largest grid (the whole shard,
 or a ring shard's interior rows), the warm-up pass's dropped.  The CSVs are
-copied to profiles/<tag>_pmc/.
+copied to profiles/<tag>_pmc/; keys already in profiles/pmc_launch.json and
+not measured in this run are kept.
 
     python3 scripts/pmc_launch.py [gpurun_out/pmc] [tag]
 """
@@ -53,7 +54,11 @@ def main_launches(path):
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "pmc")
     tag = sys.argv[2] if len(sys.argv) > 2 else "r02"
+    path = os.path.join(ROOT, "profiles", "pmc_launch.json")
     out = {}
+    if os.path.exists(path):  # earlier runs' keys stay; keys measured again are replaced
+        with open(path) as f:
+            out = json.load(f)
     keys = sorted({d.split("__")[0] for d in os.listdir(src) if "__" in d and os.path.isdir(os.path.join(src, d))})
     for key in keys:
         shape, mode, g, h = key.split("_")
@@ -93,7 +98,6 @@ def main():
         os.makedirs(dst, exist_ok=True)
         for p, c in csvs.items():
             shutil.copy(c, os.path.join(dst, f"{key}__{p}.csv"))
-    path = os.path.join(ROOT, "profiles", "pmc_launch.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     for k, v in sorted(out.items()):

@@ -25,7 +25,7 @@ def make_group(W, H, n, topology="torus", rule="life", gpp=0, seed=77, cells=Non
 
 
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
-@pytest.mark.parametrize("gpp", [1, 2, 6])
+@pytest.mark.parametrize("gpp", [1, 2, 6, 12])
 def test_group_torus_matches_oracle(gpu, n, gpp):
     W, H, gens = 32 * 300, 83, 13  # uneven shards (83 rows over n), rows <= 2G for some
     shards, g, full = make_group(W, H, n, gpp=gpp)

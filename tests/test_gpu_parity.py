@@ -27,7 +27,7 @@ def rule_obj(rule):
     return Rule(rule[0], rule[1])
 
 
-GPP = [1, 2, 3, 4, 5, 8]  # generations fused per HBM pass (temporal blocking depth)
+GPP = [1, 2, 3, 4, 5, 8, 10, 12]  # generations fused per HBM pass (temporal blocking depth)
 
 
 def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, band=0, gpp=1,
@@ -118,7 +118,7 @@ def test_torus_named_rules(gpu, name, gpp):
     check_run(32 * 96, 31, 10, RULES[name], "torus", seed=3, gpp=gpp)
 
 
-@pytest.mark.parametrize("gpp", [1, 2, 3, 4, 6, 7, 8])
+@pytest.mark.parametrize("gpp", [1, 2, 3, 4, 6, 7, 8, 9, 11, 12])
 @pytest.mark.parametrize("vec", [1, 2, 4])
 def test_words_per_lane(gpu, vec, gpp):
     # every lane width at every depth, full and partial strips, torus and clipped
@@ -132,7 +132,7 @@ def test_words_per_lane(gpu, vec, gpp):
 def test_tuning_rejects_bad_values(gpu):
     from gameoflife import _native as N
     with engine(32 * 6, 8) as e:
-        for kw in [dict(gens_per_pass=9), dict(words_per_lane=3), dict(words_per_lane=4),
+        for kw in [dict(gens_per_pass=13), dict(words_per_lane=3), dict(words_per_lane=4),
                    dict(band_rows=-1)]:
             with pytest.raises(N.GolError):
                 e.set_tuning(**kw)
@@ -280,30 +280,28 @@ def test_known_patterns_on_gpu(gpu):
 
 def test_pass_plan(gpu):
     """gol_pass_plan: the depths cover the generations exactly, respect the
-    cap (8, or a fixed gens_per_pass), and wide boards fuse deeper passes
-    (DESIGN.md "Pass planner")."""
-    with engine(32 * 300, 64) as e:  # narrow: 8-generation passes, 6 to fill the remainder
+    cap (12 on the B3/S23 torus, 8 for other rules and the clipped topology,
+    or a fixed gens_per_pass), run deepest first, and wide boards fuse deeper
+    passes (DESIGN.md "Pass planner")."""
+    with engine(32 * 300, 64) as e:  # narrow (3 strips): 8-generation passes
         for n in (1, 5, 6, 7, 13, 50, 60, 1024):
             plan = e.pass_plan(n)
-            assert sum(plan) == n and all(1 <= g <= 8 for g in plan), (n, plan)
+            assert sum(plan) == n and all(1 <= g <= 12 for g in plan), (n, plan)
+            assert plan == sorted(plan, reverse=True), plan
         assert e.pass_plan(48) == [8] * 6
-        assert sorted(e.pass_plan(60)) == [6, 6] + [8] * 6
+        assert e.pass_plan(102) == [8] * 12 + [6]
         assert e.pass_plan(60, hashes=True) == [6] * 10  # hashed: VALU-bound, 6 is best
         e.set_tuning(gens_per_pass=4)
         assert e.pass_plan(10) == [4, 4, 2]
-    with engine(262144, 64) as e:  # wide (67 strips): 8-generation passes, 6 for the remainder
-        plan = e.pass_plan(60)
-        assert sum(plan) == 60 and sorted(plan) == [6, 6] + [8] * 6, plan
-        hplan = e.pass_plan(60, hashes=True)  # hashed passes are VALU-bound: 5 or 6
-        assert sum(hplan) == 60 and set(hplan) <= {5, 6}, hplan
+    with engine(262144, 64) as e:  # wide (67 strips): 12-generation passes
+        assert e.pass_plan(60) == [12] * 5
+        assert e.pass_plan(20) == [12, 8]
+        assert e.pass_plan(60, hashes=True) == [10] * 6  # hashed: 10 (3 waves/SIMD), 6 for remainders
+        assert e.pass_plan(20, hashes=True) == [10, 10]
         check = e.pass_plan(13)
         assert sum(check) == 13
-    with engine(32 * 64, 21) as e:  # the plan's passes step bit-exactly
-        board = O.seed_packed(32 * 64, 21, 4)
-        e.load(board)
-        got = e.step(50, hashes=True)
-        _, want = O.run_packed(board, 32 * 64, 50, O.TORUS, O.LIFE)
-        np.testing.assert_array_equal(got, want)
+    with engine(262144, 64, rule=rule_obj(O.REF_EFFECTIVE)) as e:  # other rules: planned passes stop at 8
+        assert max(e.pass_plan(60)) <= 8 and sum(e.pass_plan(60)) == 60
 
 
 def test_snapshot_into_caller_buffer(gpu):

@@ -86,7 +86,7 @@ def test_rccl_ring_matches_oracle(gpu, world, topology, gpp):
 
 @pytest.mark.parametrize("Hs,gpp,hashed", [(97, 1, True), (203, 6, True), (203, 8, True), (203, 8, False),
                                            (203, 0, True), (203, 0, False), (12, 8, True), (5, 8, True),
-                                           (301, 3, False)])
+                                           (301, 3, False), (203, 12, True), (203, 10, False), (12, 12, True)])
 def test_rccl_self_ring_matches_oracle(gpu, Hs, gpp, hashed):
     from gameoflife import _native as N
     from gameoflife.engine import GolEngine
@@ -98,7 +98,7 @@ def test_rccl_self_ring_matches_oracle(gpu, Hs, gpp, hashed):
         e.load(board)
         e.comm_init(N.unique_id(), 0, 1)
         plan = e.pass_plan(gens, hashes=hashed)
-        assert max(plan) <= min(8, Hs) and sum(plan) == gens
+        assert max(plan) <= min(12, Hs) and sum(plan) == gens
         got = e.step(gens, hashes=hashed)
         if hashed:
             np.testing.assert_array_equal(e.allreduce_u64(got), want)

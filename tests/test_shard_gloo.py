@@ -89,7 +89,7 @@ def _worker(rank, world, port, torus, gpp, out_q):
 
 
 @pytest.mark.parametrize("world,torus,gpp", [(2, True, 1), (2, True, 8), (3, True, 6), (3, True, 8),
-                                             (2, False, 3), (3, False, 8)])
+                                             (2, False, 3), (3, False, 8), (2, True, 12), (3, True, 12)])
 def test_sharded_matches_unsharded(world, torus, gpp):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -125,6 +125,7 @@ def test_combine_hashes_wraps_mod_2_64():
 def test_ring_depth_cap_mirrors_libgol():
     """floor(H / N) caps a ring's passes (every rank sends the same G rows);
     a 1-rank self-ring sends its own G rows, so G <= H."""
-    assert ring_depth_cap(37, 3) == 8 and ring_depth_cap(37, 5) == 7 and ring_depth_cap(5, 1) == 5
-    assert ring_depth_cap(262144, 8) == 8 and ring_depth_cap(262144, 8, 6) == 6
+    assert ring_depth_cap(37, 3) == 12 and ring_depth_cap(37, 5) == 7 and ring_depth_cap(5, 1) == 5
+    assert ring_depth_cap(262144, 8) == 12 and ring_depth_cap(262144, 8, 6) == 6
+    assert ring_depth_cap(262144, 8, life_torus=False) == 8 and ring_depth_cap(262144, 8, 10, False) == 10
     assert fixed_depth_plan(13, 8) == [8, 5] and fixed_depth_plan(12, 6) == [6, 6]
