@@ -278,6 +278,16 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
     // the plain choice (137 rows, no tail) and 0.0471 for 256 rows without
     // the tail; at G = 6 the plain choice stays best.
     if (strips < 32 && gens >= 7 && resident > 0) return (int)std::min<int64_t>(256, std::max<int64_t>(rows, 1));
+    // Wide boards at 10- to 12-generation passes (3 waves per SIMD, 2G halo
+    // rows per band): 384-row bands when that is still >= 3 rounds of
+    // resident waves, else 256, both with the tail split.  Same-box sweep at
+    // G = 12 (profiles/r02_deep_band_sweep.txt, 4 rounds, ms per generation):
+    // 262144^2 0.5660 (384) vs 0.5821 (the plain choice), x 131072 0.2882 vs
+    // 0.2926, x 65536 0.1464 vs 0.1483, x 32768 0.0745 (256) vs 0.0761.
+    if (strips >= 32 && gens >= 10 && resident > 0) {
+        const int64_t waves384 = (rows + 383) / 384 * strips;
+        return (int)std::min<int64_t>(waves384 >= 3 * resident ? 384 : 256, std::max<int64_t>(rows, 1));
+    }
     if (resident > 0 && strips >= 32) {
         auto cost = [&](int64_t b) -> double {
             const int64_t waves = (rows + b - 1) / b * strips;

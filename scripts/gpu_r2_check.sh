@@ -1,0 +1,8 @@
+# GPU test suite, then the driver's bench command (N = 1).
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_20.json 2> gpurun_out/bench_20.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_20.json; exit $rc
