@@ -27,7 +27,7 @@ def main():
                 for G in range(1, maxg + 1):
                     gens = 24 if 24 % G == 0 else G * (24 // G + 1)
                     gens = max(gens, 2 * G)
-                    e.set_tuning(gens_per_pass=G)
+                    e.set_tuning(gens_per_pass=G, words_per_lane=int(os.environ.get("WPL", "0")))
                     e.seed(0x5EED)
                     e.step(6)
                     e.profile(True)
