@@ -309,15 +309,16 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     ncclSend/ncclRecv to itself, then the boundary rows on the edge stream).
     (1) the whole board, (2) one rank's shard of the N = 8 decomposition
     (262144 x 32768): what each of 8 ranks computes, without the xGMI latency
-    of a real ring.  Both with >= 48 warm-up generations: after the GPU idles
-    (here: the shard's allocation) the first ~20 launches run 10-25 % slower
-    while the power management settles (profiles/r02_warmup_curve.txt), which
-    a 6-generation warm-up of a 0.08 ms-per-generation shard does not cover."""
+    of a real ring.  Both after 50 ms of untimed steps: after the GPU idles
+    (here: the shard's allocation) the first ~15-20 ms of launches run 10-25 %
+    slower while the power management settles (profiles/r02_warmup_curve.txt),
+    which a few generations of a 0.08 ms-per-generation shard do not cover."""
     out = {}
-    warm = max(a.warmup, 48)
+    warm = "50 ms settled"
     eng.comm_init(N.unique_id(), 0, 1)
     eng.seed(0x5EED)
-    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, warm, False)
+    settle(eng, 50.0, False, 12)
+    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
     out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
                                     "warmup": warm, "ms_per_step": round(dt / a.steps * 1e3, 4),
                                     "pass_plan": eng.pass_plan(min(a.steps, 1024))}
@@ -325,7 +326,8 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     with GolEngine(W, H, topology="torus", rule="life", device=local, row0=0, rows=rows8) as e8:
         e8.comm_init(N.unique_id(), 0, 1)  # a 1-rank ring over a shard-sized torus
         e8.seed(0x5EED)
-        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, warm, False)
+        settle(e8, 50.0, False, 12)
+        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         plan8 = e8.pass_plan(min(a.steps, 1024))
     out["per_rank_shard_self_ring"] = {
         "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
