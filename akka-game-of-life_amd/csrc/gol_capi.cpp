@@ -257,7 +257,11 @@ int lane_words(const gol_ctx* ctx, int gens) {
 // `resident`: waves the whole GPU holds at once for this kernel (0: unknown).
 int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t resident) {
     if (ctx->band_rows > 0) return ctx->band_rows;
-    if (gens == 1) return 16;  // short bands: more waves in flight, seams hit the Infinity Cache
+    // Single-generation passes: 4-row bands -- more, shorter streams in
+    // flight; the band seams (2 halo rows per 4) hit the Infinity Cache.
+    // Same-box sweep (profiles/r02_g1_band_sweep.txt, ms per generation):
+    // 65536^2 0.197 (4) vs 0.209 (16), 262144^2 3.12 vs 3.45, x 32768 0.395 vs 0.420.
+    if (gens == 1) return 4;
     // Multi-generation passes recompute 2G halo rows per band: keep bands
     // >= 64 rows, aim at ~8192 waves, cap at 256 rows.
     const int64_t bands = std::max<int64_t>(1, 8192 / std::max(1, strips));
