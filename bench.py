@@ -184,6 +184,17 @@ def valu_peak_gcups(mix, clock_ghz):
     return SIMDS * clock_ghz * 1e9 / cycles * CELLS_PER_WAVE_INSTR / 1e9, cycles
 
 
+def compact_plan(plan):
+    """A long pass plan as "n x G" runs, e.g. "128 x 8" or "7 x 12 + 2 x 9"."""
+    runs = []
+    for g in plan:
+        if runs and runs[-1][1] == g:
+            runs[-1][0] += 1
+        else:
+            runs.append([1, g])
+    return " + ".join(f"{n} x {g}" for n, g in runs)
+
+
 def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False):
     """Roofline of the dominant kernel (see the module docstring)."""
     if not launches:
@@ -193,7 +204,7 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
     gcups = cells * gpl / avg_s / 1e9
     algo = cells * gpl * BYTES_PER_CELL_UPDATE
     common = {"avg_launch_ms": round(avg_s * 1e3, 4), "launches": launches, "generations_per_launch": gpl,
-              "pass_plan": plan}
+              "pass_plan": plan if len(plan) <= 16 else compact_plan(plan)}
     pmc = plan_pmc(shape, mode, plan, hashed)
     if set(plan) == {1}:  # single-generation passes: a stream over the plane, HBM-bound
         r = {"bound": "hbm", "achieved": round(algo / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

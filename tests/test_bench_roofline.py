@@ -49,3 +49,8 @@ def test_hashed_mix_adds_the_multiply_add():
     p0, c0 = bench.valu_peak_gcups(bench.VALU_MIX, 2.4)
     p1, c1 = bench.valu_peak_gcups(bench.VALU_MIX_HASH, 2.4)
     assert abs(c1 - c0 - 4.6) < 1e-9 and p1 < p0
+
+
+def test_compact_plan_keeps_json_short():
+    assert bench.compact_plan([1] * 256) == "256 x 1"
+    assert bench.compact_plan([12] * 7 + [9, 9]) == "7 x 12 + 2 x 9"
