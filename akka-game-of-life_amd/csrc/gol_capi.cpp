@@ -642,14 +642,16 @@ int depth_cap(const gol_ctx* ctx) {
 // (profiles/r02_plan_mix_ab.txt: 20 generations 12 + 8 at 111.1k GCUPS vs
 // 6 + 6 + 8 at 103.6k; 60 generations 5 x 12 at 119.0k vs 6 x 10 at 115.0k).
 // With the fused per-generation hash the kernels are VALU-bound from G = 6
-// on; per generation 6 and 10 are best on wide boards, 6 on narrow ones
-// (HASH=1 rows; G >= 11 hashed drops to 2-3 waves/SIMD).
+// on; since the hashed G = 7..9 instances skip the dead pipeline-fill steps
+// too (no spill with the LDS hash sums), 8 is best per generation on both
+// wide and narrow boards (HASH=1 rows, profiles/r02_hash_peel_ab.txt; G >= 11
+// hashed drops to 2 waves/SIMD).
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
     // [hashed][wide]; G = 0 .. 12
     {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26, 1.457, 1.657, 1.829, 1.995},    // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
      {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231, 1.37, 1.52, 1.70, 1.77}},        // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
-    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.262, 1.475, 1.627, 1.788, 2.365, 2.547},  // narrow, hashed (65536^2)
-     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.186, 1.395, 1.516, 1.645, 2.20, 2.30}}};  // wide, hashed (262144^2)
+    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.09, 1.20, 1.49, 1.70, 2.365, 2.547},      // narrow, hashed (65536^2)
+     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.125, 1.27, 1.46, 1.645, 2.20, 2.30}}};    // wide, hashed (262144^2)
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);

@@ -921,13 +921,18 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 
 #pragma unroll
         for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
+#ifndef GOL_HASH_PEEL_MAXG
+#define GOL_HASH_PEEL_MAXG 9
+#endif
         constexpr int kFill = (2 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
         // The peeled fill is one long straight-line block; only the B3/S23
         // instances keep their rings in registers through it (the generic-rule
-        // mux tree, and the per-generation hash sums at G > 6, make the
-        // scheduler spill), so they alone skip the dead fill steps.
+        // mux tree makes the scheduler spill, and so do the hashed instances
+        // at G >= 10: 1.4 KB of scratch), so they alone skip the dead fill
+        // steps.  Hashed G = 8 peeled: 122 VGPRs, no spill (unpeeled: 128
+        // forced + 4 dwords spilled).
         int q_begin = 0;
-        if constexpr (LIFE && (!HASH || G <= 6)) {
+        if constexpr (LIFE && (!HASH || G <= GOL_HASH_PEEL_MAXG)) {
             static_for<kFill>([&](auto Q) { row_step(Q.value, Q.value % kMRing, true); });
             q_begin = kFill;
         }

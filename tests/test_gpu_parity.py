@@ -290,14 +290,14 @@ def test_pass_plan(gpu):
             assert plan == sorted(plan, reverse=True), plan
         assert e.pass_plan(48) == [8] * 6
         assert e.pass_plan(102) == [8] * 12 + [6]
-        assert e.pass_plan(60, hashes=True) == [6] * 10  # hashed: VALU-bound, 6 is best
+        assert e.pass_plan(60, hashes=True) == [8] * 4 + [7] * 4  # hashed: VALU-bound, 7-8 are best
         e.set_tuning(gens_per_pass=4)
         assert e.pass_plan(10) == [4, 4, 2]
     with engine(262144, 64) as e:  # wide (67 strips): 12-generation passes
         assert e.pass_plan(60) == [12] * 5
         assert e.pass_plan(20) == [12, 8]
-        assert e.pass_plan(60, hashes=True) == [10] * 6  # hashed: 10 (3 waves/SIMD), 6 for remainders
-        assert e.pass_plan(20, hashes=True) == [10, 10]
+        assert e.pass_plan(60, hashes=True) == [8] * 4 + [7] * 4  # hashed: 7-8 (4 waves/SIMD)
+        assert e.pass_plan(20, hashes=True) == [7, 7, 6]
         check = e.pass_plan(13)
         assert sum(check) == 13
     with engine(262144, 64, rule=rule_obj(O.REF_EFFECTIVE)) as e:  # other rules: planned passes stop at 8
