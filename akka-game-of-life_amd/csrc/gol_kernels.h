@@ -24,6 +24,15 @@ constexpr uint32_t kHashRowMul = 0x9E3779B1u;
 constexpr uint32_t kHashOddAdd = 0x6A09E666u;
 constexpr uint32_t kHashPairAdd = 0x7F4A7C15u;
 
+// hipGetLastError() after a launch also returns an error left behind by any
+// earlier runtime call of this thread whose status its caller discarded (an
+// occupancy query, a teardown call, another library's probe), which would
+// then be pinned on the launch.  Every launch helper therefore drops such a
+// stale status first (reported once per error code on stderr) so its check
+// reports the launch alone; a device fault still surfaces at the next
+// synchronising call, which every entry point checks.
+void drop_stale_error();
+
 __host__ __device__ __forceinline__ uint32_t hash_row_key(int64_t y) {
     const uint32_t t = (uint32_t)y * kHashRowMul;
     return ((t ^ (t >> 15)) << 1) | 1u;

@@ -967,6 +967,7 @@ constexpr bool kHgLanes = VEC <= 2;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
+    drop_stale_error();
     if constexpr (G == 1) {
         hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
                            dim3(kWaveLanes * kWavesPerWG), 0, st, p);
