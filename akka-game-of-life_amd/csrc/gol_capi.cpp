@@ -642,16 +642,19 @@ int depth_cap(const gol_ctx* ctx) {
 // (profiles/r02_plan_mix_ab.txt: 20 generations 12 + 8 at 111.1k GCUPS vs
 // 6 + 6 + 8 at 103.6k; 60 generations 5 x 12 at 119.0k vs 6 x 10 at 115.0k).
 // With the fused per-generation hash the kernels are VALU-bound from G = 6
-// on; since the hashed G = 7..9 instances skip the dead pipeline-fill steps
-// too (no spill with the LDS hash sums), 8 is best per generation on both
-// wide and narrow boards (HASH=1 rows, profiles/r02_hash_peel_ab.txt; G >= 11
-// hashed drops to 2 waves/SIMD).
+// on.  The hashed B3/S23 instances skip the dead pipeline-fill steps up to
+// G = 12 (row step force-inlined: 153 / 163 / 168 VGPRs at G = 10 / 11 / 12,
+// 3 waves per SIMD, G = 12 with a 7-dword spill), so on wide boards G = 10
+// and 11 are best per generation (same-box sweep, profiles/r02_hash_deep_ab.txt:
+// 0.72 / 0.70 ms per generation at 262144^2 vs 0.73 at G = 8; 20 generations
+// as 10 + 10 94.5k vs 7 + 7 + 6 90.4k GCUPS); narrow boards stay at 8
+// (HASH=1 rows; profiles/r02_hash_peel_ab.txt, r02_hash_deep_ab.txt).
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
     // [hashed][wide]; G = 0 .. 12
     {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26, 1.457, 1.657, 1.829, 1.995},    // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
      {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231, 1.37, 1.52, 1.70, 1.77}},        // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
-    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.09, 1.20, 1.49, 1.70, 2.365, 2.547},      // narrow, hashed (65536^2)
-     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.125, 1.27, 1.46, 1.645, 2.20, 2.30}}};    // wide, hashed (262144^2)
+    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.09, 1.20, 1.49, 1.60, 1.75, 2.49},        // narrow, hashed (65536^2)
+     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.08, 1.22, 1.40, 1.51, 1.63, 1.97}}};      // wide, hashed (262144^2)
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);

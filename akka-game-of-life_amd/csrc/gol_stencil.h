@@ -789,8 +789,12 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
 #ifndef GOL_HG_MINWAVES8
 #define GOL_HG_MINWAVES8 4
 #endif
+#ifndef GOL_HG_MINWAVES_DEEP
+#define GOL_HG_MINWAVES_DEEP 3
+#endif
 template <int VEC, int G, bool LIFE, bool HASH>
-constexpr int kHgMinWaves = (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8 : 1;
+constexpr int kHgMinWaves = (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8
+                             : (VEC == 2 && G >= 10 && LIFE && HASH) ? GOL_HG_MINWAVES_DEEP : 1;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH>)) void multistep_hg_kernel(
@@ -879,7 +883,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         // built from the clamped rows before the band and are never stored,
         // hashed or read by a valid row), so the pipeline fill -- the first
         // kFill rows, q known at compile time -- skips those stage steps.
-        auto row_step = [&](const int q, const int u, const bool fill) {
+        auto row_step = [&](const int q, const int u, const bool fill) __attribute__((always_inline)) {
             load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
             if constexpr (HASH) {
 #pragma unroll
@@ -922,7 +926,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 #pragma unroll
         for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
 #ifndef GOL_HASH_PEEL_MAXG
-#define GOL_HASH_PEEL_MAXG 9
+#define GOL_HASH_PEEL_MAXG 12
 #endif
         constexpr int kFill = (2 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
         // The peeled fill is one long straight-line block; only the B3/S23
@@ -933,7 +937,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         // forced + 4 dwords spilled).
         int q_begin = 0;
         if constexpr (LIFE && (!HASH || G <= GOL_HASH_PEEL_MAXG)) {
-            static_for<kFill>([&](auto Q) { row_step(Q.value, Q.value % kMRing, true); });
+            static_for<kFill>([&](auto Q) __attribute__((always_inline)) { row_step(Q.value, Q.value % kMRing, true); });
             q_begin = kFill;
         }
         for (int q0 = q_begin; q0 < n_in; q0 += kMRing) {

@@ -3,7 +3,7 @@
 * 262144^2 torus (BASELINE.json configs[3], 8 GiB per plane), 20 generations
   -- the driver's `bench.py --steps 20`: unhashed the planner runs 12 + 8
   (the wide G = 12 and G = 8 instances of multistep_hg_kernel, tail split
-  active at >= 32 strips), hashed the planner's hashed plan (7 + 7 + 6).
+  active at >= 32 strips), hashed the planner's hashed plan (10 + 10).
   As one context (N = 1), as an in-process group of 8 row shards of 32768 rows (the N = 8 decomposition:
   interior launch + boundary rows on the edge stream), and as a 1-rank RCCL
   self-ring (the ring schedule's ncclSend / ncclRecv).
@@ -44,7 +44,7 @@ def test_full_size_262144_plans_are_the_benchs(gpu):
     from gameoflife.engine import GolEngine
     with GolEngine(W, H) as e:
         assert e.pass_plan(GENS) == [12, 8]
-        assert e.pass_plan(GENS, hashes=True) == [7, 7, 6]
+        assert e.pass_plan(GENS, hashes=True) == [10, 10]
 
 
 def test_full_size_262144_one_context(gpu, oracle_run):

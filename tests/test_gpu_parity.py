@@ -296,8 +296,8 @@ def test_pass_plan(gpu):
     with engine(262144, 64) as e:  # wide (67 strips): 12-generation passes
         assert e.pass_plan(60) == [12] * 5
         assert e.pass_plan(20) == [12, 8]
-        assert e.pass_plan(60, hashes=True) == [8] * 4 + [7] * 4  # hashed: 7-8 (4 waves/SIMD)
-        assert e.pass_plan(20, hashes=True) == [7, 7, 6]
+        assert e.pass_plan(60, hashes=True) == [11] * 4 + [8] * 2  # hashed: 10-11 best (3 waves/SIMD)
+        assert e.pass_plan(20, hashes=True) == [10, 10]
         check = e.pass_plan(13)
         assert sum(check) == 13
     with engine(262144, 64, rule=rule_obj(O.REF_EFFECTIVE)) as e:  # other rules: planned passes stop at 8
