@@ -140,7 +140,7 @@ __device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VE
 // row and the hardware bounds check drops the store.  No exec-mask branch
 // around the store, so the counted vmcnt waits of the loads that follow stay
 // exact (a skippable store makes the compiler wait for the worse path).
-template <int VEC>
+template <int VEC, bool NT = (GOL_NT_STORES != 0)>
 __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t row_bytes, int col, bool lane_ok,
                                           const Words<VEC>& d) {
     const __amdgpu_buffer_rsrc_t rs =
@@ -148,12 +148,12 @@ __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t ro
     const int voff = lane_ok ? col * 4 : 0x7FFFFFF0;
     if constexpr (VEC == 4) {
         const U32x4 v = {d.w[0], d.w[1], d.w[2], d.w[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, GOL_NT_STORES ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, NT ? 2 : 0);
     } else if constexpr (VEC == 2) {
         const U32x2 v = {d.w[0], d.w[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, 0, GOL_NT_STORES ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, 0, NT ? 2 : 0);
     } else {
-        __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, GOL_NT_STORES ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b32(d.w[0], rs, voff, 0, NT ? 2 : 0);
     }
 }
 
@@ -438,6 +438,18 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
 // --------------------------------------------------------------------------
 // One generation per pass.
 // --------------------------------------------------------------------------
+// Single-generation passes store non-temporally: the next plane is not
+// re-read by this pass, and with the 4-row bands the store stream competes
+// with the halo re-reads for the caches.  Same-box A/B
+// (profiles/r02_g1_nt_ab.txt, 3 rounds): 65536^2 0.1963 -> 0.1891 ms,
+// 262144^2 3.129 -> 3.003 ms, 262144 x 32768 0.399 -> 0.383 ms per
+// generation.  The multi-generation kernels keep plain stores (round 1:
+// -3..-8 % at G = 6 with non-temporal stores, profiles/r01_bandwidth.txt).
+#ifndef GOL_G1_NT_STORES
+#define GOL_G1_NT_STORES 1
+#endif
+constexpr bool kG1NtStores = GOL_NT_STORES || GOL_G1_NT_STORES;
+
 template <int VEC, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
     const int lane = threadIdx.x & (kWaveLanes - 1);
@@ -529,7 +541,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
             }
             const int r = out_of(i);
-            store_row<VEC>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
+            store_row<VEC, kG1NtStores>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
             if constexpr (HASH) {
                 if (in_band) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc);
             }
