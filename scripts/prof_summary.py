@@ -53,7 +53,8 @@ def main():
         json.dump(benches, f, indent=1)
 
     trace = rows(os.path.join(prof, "bench_trace", "bench_kernel_trace.csv"))
-    groups = defaultdict(list)
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+    groups = defaultdict(list)  # (kernel, grid) -> durations in dispatch order
     for r in trace:
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         groups[(r["Kernel_Name"], int(r["Grid_Size_X"]), int(r["Grid_Size_Y"]))].append(dur)
@@ -72,29 +73,40 @@ def main():
             return f"step_kernel<2, true, {h}, false, true>"
         return f"multistep_hg_kernel<2, {G}, true, {h}, false, true>"
 
-    def traced(plan, hashed):
-        # the plan's launches at the largest grid of each instance: the
-        # whole-board launches (warm-up launches of the same depth included)
-        tot, n = 0.0, 0
+    def traced(plan, hashed, warmup):
+        # The timed launches of a run: in dispatch order, each depth's first
+        # launches at the largest grid of its instance (the whole-board
+        # launch), after the warm-up's single pass of `warmup` generations
+        # (gol_step plans <= 12 generations as one pass).  Returns (mean of
+        # the timed launches, mean over every launch of those instances).
+        seen = defaultdict(int)
+        if warmup and warmup <= 12:
+            seen[warmup] = 1
+        timed, every = [], []
         for G in plan:
             cands = [(gx, d) for (name, gx, gy), d in groups.items() if instance(G, hashed) in name]
             if not cands:
-                return None
-            gx, d = max(cands)
-            tot += statistics.mean(d)
-            n += 1
-        return tot / n
+                return None, None
+            gx, d = max(cands, key=lambda c: c[0])
+            if seen[G] >= len(d):
+                return None, None
+            timed.append(d[seen[G]])
+            seen[G] += 1
+            every.append(statistics.mean(d))
+        return statistics.mean(timed), statistics.mean(every)
 
     for label, rec, hashed in (("main workload", b, False), ("with_state_hash", b.get("with_state_hash"), True)):
         if not rec or not rec.get("roofline"):
             continue
         ro = rec["roofline"]
         plan = rec.get("pass_plan") or ro.get("pass_plan") or b.get("pass_plan")
-        t = traced(plan, hashed) if plan else None
+        t, t_all = traced(plan, hashed, b.get("warmup")) if plan else (None, None)
         lines.append(f"  {label:16s} bench avg_launch_ms={ro.get('avg_launch_ms')} launches={ro.get('launches')}"
-                     + (f"   rocprof plan-weighted mean={t:.4f} ms" if t else ""))
-    lines.append("(rocprof's per-instance means also hold the warm-up launches and the N = 1 ring-schedule runs'")
-    lines.append(" launches of the same instance and grid; the bench's numbers are its timed launches only)")
+                     + (f"   rocprof, the same timed launches: mean={t:.4f} ms"
+                        f" (every launch of those instances and grids: {t_all:.4f} ms)" if t else ""))
+    lines.append("(the timed launches are picked from the trace in dispatch order: each pass depth's first")
+    lines.append(" whole-board launches after the warm-up pass; the instances' later launches at the same grid")
+    lines.append(" belong to the N = 1 ring-schedule runs on a settled, sparser board)")
     with open(os.path.join(dst, f"{tag}_kernel_trace.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
