@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[3], DESIGN.md "Measurement"): a 262144 x
 262144 torus, B3/S23, Bernoulli(0.5) splitmix64 board (seed 0x5EED),
 row-sharded over N GPUs (strong scaling; N = 1 runs the whole board on one
-GPU).  A "step" is one generation of the whole board.  At N = 1 the
-single-GPU roofline run of configs[2] (65536^2) is measured too and reported
+GPU).  A "step" is one generation of the whole board.  Every GPU also runs
+the single-GPU roofline case of configs[2] (65536^2) before the timed
+262144^2 window -- the same sequence at every N -- and rank 0 reports it
 under "secondary".
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
@@ -373,10 +374,17 @@ def main():
     from gameoflife.engine import GolEngine
 
     W = H = a.board
-    # configs[2] (65536^2, N = 1 only) first: a board allocated after the
-    # 16 GiB one was freed stepped ~5 % slower (scripts/alloc_order.py).
+    # Every GPU runs the same sequence at every N: the 65536^2 measurement
+    # (BASELINE.json configs[2]) first, then the 262144^2 workload.  At N = 1
+    # the 65536^2 board comes first because a board allocated after the
+    # 16 GiB one was freed stepped ~5 % slower (scripts/alloc_order.py); at
+    # N > 1 each rank creates its shard and its RCCL communicator first (the
+    # communicator setup idles the GPU for up to a second), then runs the same
+    # 65536^2 measurement, so the sharded window starts from a GPU as busy as
+    # the N = 1 window does (after an idle gap the first ~15-20 ms of launches
+    # run 10-25 % slower, profiles/r02_warmup_curve.txt).
     secondary = None
-    if rank == 0 and world == 1 and not a.no_secondary:
+    if world == 1 and not a.no_secondary:
         secondary = secondary_run(GolEngine, torch, dist, a, local)
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
@@ -386,6 +394,9 @@ def main():
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         eng.comm_init(bytes(t.tolist()), rank, world)
+        if not a.no_secondary:
+            secondary = secondary_run(GolEngine, torch, dist, a, local)
+            secondary["note"] = f"measured on rank {rank}'s GPU; each of the {world} ranks ran it on its own GPU"
     eng.seed(0x5EED)
 
     dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
@@ -443,11 +454,10 @@ def main():
         out["ring_schedule_n1"] = ring
     eng.close()
 
-    if rank == 0 and world == 1:
-        if secondary is not None:
-            out["secondary"] = secondary
-        if not a.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
+    if rank == 0 and secondary is not None:
+        out["secondary"] = secondary
+    if rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(out) + "\n").encode())
