@@ -337,18 +337,21 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     rows8 = H // 8
     with GolEngine(W, H, topology="torus", rule="life", device=local, row0=0, rows=rows8) as e8:
         e8.comm_init(N.unique_id(), 0, 1)  # a 1-rank ring over a shard-sized torus
-        # First as an N = 8 rank meets the driver's window: the GPU idle
-        # while the ranks initialise RCCL, then seed, W warm-up steps and the
-        # timed steps -- inside the clock's recovery, like the N = 1 line's
-        # own window (no settle), so the two compare directly.
+        # First as an N = 8 rank meets the driver's window (main(), N > 1):
+        # the GPU idle while the ranks initialise RCCL, the 65536^2 run, then
+        # seed, W warm-up steps and the timed steps, no settle -- like the
+        # N = 1 line's own window, so the two compare directly.
         time.sleep(1.0)
+        if not a.no_secondary:
+            secondary_run(GolEngine, torch, dist, a, local)
         e8.seed(0x5EED)
         dtf, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         out["per_rank_shard_driver_window"] = {
             "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dtf / 1e9, 2),
             "unit": "GCUPS", "warmup": a.warmup, "ms_per_step": round(dtf / a.steps * 1e3, 4),
-            "note": "1 s idle, seed, warm-up and timed steps as in an N = 8 rank's run; x 8 / the N = 1 value "
-                    "is the per-cell efficiency that run can reach before any xGMI cost"}
+            "note": "an N = 8 rank's sequence on this GPU (1 s idle for the communicator setup, the 65536^2 run, "
+                    "seed, W warm-up and K timed steps); x 8 / the N = 1 value is the per-cell efficiency that "
+                    "run can reach before any xGMI cost"}
         e8.seed(0x5EED)
         settle(e8, 50.0, False, 12)
         dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
