@@ -69,6 +69,14 @@ struct gol_ctx {
     hipStream_t compute = nullptr, comm = nullptr;
     hipStream_t edge = nullptr;  // boundary-row kernels of a sharded pass (concurrent with the interior)
     hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_edge = nullptr;
+    // asynchronous snapshot (gol_snapshot_async / gol_snapshot_wait): the
+    // board at the snapshot epoch, row-major, copied to the host on `xfer`
+    // while later passes run on `compute`
+    uint32_t* snap = nullptr;
+    hipStream_t xfer = nullptr;
+    hipEvent_t ev_snap_ready = nullptr, ev_snap_done = nullptr;
+    bool snap_pending = false;
+    uint64_t snap_epoch = 0;
     // RCCL
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
@@ -704,6 +712,7 @@ void destroy_impl(gol_ctx* c) {
     if (c->compute) hipStreamSynchronize(c->compute);
     if (c->comm) hipStreamSynchronize(c->comm);
     if (c->edge) hipStreamSynchronize(c->edge);
+    if (c->xfer) hipStreamSynchronize(c->xfer);
     if (c->nccl) ncclCommDestroy(c->nccl);
     for (auto& e : c->evs) {
         if (e.start) hipEventDestroy(e.start);
@@ -712,6 +721,9 @@ void destroy_impl(gol_ctx* c) {
     if (c->ev_ready) hipEventDestroy(c->ev_ready);
     if (c->ev_halo) hipEventDestroy(c->ev_halo);
     if (c->ev_edge) hipEventDestroy(c->ev_edge);
+    if (c->ev_snap_ready) hipEventDestroy(c->ev_snap_ready);
+    if (c->ev_snap_done) hipEventDestroy(c->ev_snap_done);
+    if (c->snap) hipFree(c->snap);
     for (auto* p : c->plane) if (p) hipFree(p);
     if (c->halo_top) hipFree(c->halo_top);
     if (c->halo_bot) hipFree(c->halo_bot);
@@ -720,6 +732,7 @@ void destroy_impl(gol_ctx* c) {
     if (c->compute) hipStreamDestroy(c->compute);
     if (c->comm) hipStreamDestroy(c->comm);
     if (c->edge) hipStreamDestroy(c->edge);
+    if (c->xfer) hipStreamDestroy(c->xfer);
     delete c;
 }
 
@@ -1100,6 +1113,81 @@ int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words) {
                                     ctx->rows, hipMemcpyDeviceToHost, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     return GOL_OK;
+}
+
+// Asynchronous snapshot: the board is copied on the device (de-interleaved
+// for the pair layout) into `snap` in the compute stream's order -- so later
+// passes cannot overwrite it first -- and from there to the host on the
+// transfer stream, concurrently with the passes queued after it.
+constexpr size_t kSnapChunkBytes = 256ull << 20;
+
+int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words) {
+    if (!ctx || !packed_out) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (host_pitch_words < ctx->wwords) return set_err(ctx, GOL_EINVAL, "host pitch too small");
+    if (ctx->snap_pending) return set_err(ctx, GOL_ESTATE, "a snapshot is in flight: call gol_snapshot_wait first");
+    if (int rc = bind(ctx)) return rc;
+    // The device copy is packed (wwords per row, no pitch padding), so the
+    // transfer of a packed host buffer is one linear copy: a 2D
+    // device-to-host copy did not overlap the passes queued after it.
+    const size_t bytes = (size_t)ctx->rows * ctx->wwords * sizeof(uint32_t);
+    if (!ctx->snap) {
+        if (hipMalloc(&ctx->snap, bytes) != hipSuccess) {
+            ctx->snap = nullptr;
+            return set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes for the snapshot buffer failed", bytes);
+        }
+        HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->xfer, hipStreamNonBlocking));
+        HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_ready, hipEventDisableTiming));
+        HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_done, hipEventDisableTiming));
+    }
+    const uint32_t* src = ctx->plane[ctx->cur];
+    if (ctx->pairs)
+        HIP_CHECK(ctx, gol::launch_convert(src, ctx->snap, ctx->pitch, ctx->wwords, (int32_t)ctx->rows, false,
+                                           ctx->compute, ctx->wwords));
+    else
+        HIP_CHECK(ctx, hipMemcpy2DAsync(ctx->snap, (size_t)ctx->wwords * 4, src, ctx->pitch * 4,
+                                        (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyDeviceToDevice, ctx->compute));
+    HIP_CHECK(ctx, hipEventRecord(ctx->ev_snap_ready, ctx->compute));
+    HIP_CHECK(ctx, hipStreamWaitEvent(ctx->xfer, ctx->ev_snap_ready, 0));
+    if (host_pitch_words == ctx->wwords) {
+        // in chunks (GOL_SNAP_CHUNK_MB, 0 = one copy): see DESIGN.md section 2
+        const char* env = getenv("GOL_SNAP_CHUNK_MB");
+        const size_t chunk = env ? (size_t)atol(env) << 20 : kSnapChunkBytes;
+        const size_t step = chunk ? chunk : bytes;
+        for (size_t off = 0; off < bytes; off += step)
+            HIP_CHECK(ctx, hipMemcpyAsync(reinterpret_cast<char*>(packed_out) + off,
+                                          reinterpret_cast<const char*>(ctx->snap) + off, std::min(step, bytes - off),
+                                          hipMemcpyDeviceToHost, ctx->xfer));
+    } else
+        HIP_CHECK(ctx, hipMemcpy2DAsync(packed_out, host_pitch_words * 4, ctx->snap, (size_t)ctx->wwords * 4,
+                                        (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyDeviceToHost, ctx->xfer));
+    HIP_CHECK(ctx, hipEventRecord(ctx->ev_snap_done, ctx->xfer));
+    ctx->snap_pending = true;
+    ctx->snap_epoch = ctx->epoch;
+    return GOL_OK;
+}
+
+int gol_snapshot_wait(gol_ctx* ctx, uint64_t* epoch_out) {
+    if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (!ctx->snap_pending) return set_err(ctx, GOL_ESTATE, "no snapshot in flight");
+    if (int rc = bind(ctx)) return rc;
+    ctx->snap_pending = false;
+    HIP_CHECK(ctx, hipEventSynchronize(ctx->ev_snap_done));
+    if (epoch_out) *epoch_out = ctx->snap_epoch;
+    return GOL_OK;
+}
+
+int gol_host_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return set_err(nullptr, GOL_EINVAL, "gol_host_alloc: null pointer or zero size");
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return set_err(nullptr, GOL_ENOMEM, "hipHostMalloc of %zu bytes failed", bytes);
+    }
+    return GOL_OK;
+}
+
+void gol_host_free(void* p) {
+    if (p) hipHostFree(p);
 }
 
 int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state) {

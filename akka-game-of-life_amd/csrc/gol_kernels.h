@@ -99,9 +99,10 @@ hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t w
                        int64_t grow0, int32_t rows, uint64_t seed, bool pairs, hipStream_t stream);
 
 // Row-major words <-> pair-interleaved words, `rows` rows of `wwords` (even)
-// words, `pitch` words apart in both planes (src != dst).
+// words, `pitch` words apart in the source and `dst_pitch` (<= 0: `pitch`)
+// in the destination (src != dst).
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
-                          bool to_pairs, hipStream_t stream);
+                          bool to_pairs, hipStream_t stream, int64_t dst_pitch = 0);
 
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0,
                        int32_t rows, unsigned long long* slots, hipStream_t stream);

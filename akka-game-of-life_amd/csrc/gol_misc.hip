@@ -65,8 +65,8 @@ __global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int6
     }
 }
 
-__global__ void convert_kernel(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t npairs, int32_t rows,
-                               int to_pairs) {
+__global__ void convert_kernel(const uint32_t* src, uint32_t* dst, int64_t pitch, int64_t dst_pitch, int32_t npairs,
+                               int32_t rows, int to_pairs) {
     const int64_t total = (int64_t)rows * npairs;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
@@ -80,7 +80,7 @@ __global__ void convert_kernel(const uint32_t* src, uint32_t* dst, int64_t pitch
             out.x = spread_bits(in.x) | (spread_bits(in.y) << 1);
             out.y = spread_bits(in.x >> 16) | (spread_bits(in.y >> 16) << 1);
         }
-        *reinterpret_cast<uint2*>(dst + r * pitch + c) = out;
+        *reinterpret_cast<uint2*>(dst + r * dst_pitch + c) = out;
     }
 }
 
@@ -174,13 +174,14 @@ hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t w
 }
 
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
-                          bool to_pairs, hipStream_t stream) {
+                          bool to_pairs, hipStream_t stream, int64_t dst_pitch) {
+    if (dst_pitch <= 0) dst_pitch = pitch;
     if (wwords % 2 != 0) return hipErrorInvalidValue;
     const int64_t total = (int64_t)rows * (wwords / 2);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
     drop_stale_error();
-    hipLaunchKernelGGL(convert_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, pitch, wwords / 2, rows,
-                       to_pairs ? 1 : 0);
+    hipLaunchKernelGGL(convert_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, pitch, dst_pitch, wwords / 2,
+                       rows, to_pairs ? 1 : 0);
     return hipGetLastError();
 }
 

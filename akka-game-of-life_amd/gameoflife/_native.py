@@ -77,6 +77,10 @@ _SIGNATURES = {
     "gol_sync": (_c.c_int, [_vp]),
     "gol_hash": (_c.c_int, [_vp, _u64p]),
     "gol_snapshot": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_snapshot_async": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_snapshot_wait": (_c.c_int, [_vp, _u64p]),
+    "gol_host_alloc": (_c.c_int, [_c.c_size_t, ctypes.POINTER(_vp)]),
+    "gol_host_free": (None, [_vp]),
     "gol_get_cell": (_c.c_int, [_vp, _c.c_int64, _c.c_int64, ctypes.POINTER(_c.c_int)]),
     "gol_checkpoint_bytes": (_c.c_int, [_vp, ctypes.POINTER(_c.c_size_t)]),
     "gol_checkpoint": (_c.c_int, [_vp, _vp, _c.c_size_t]),

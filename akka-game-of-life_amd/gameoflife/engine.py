@@ -83,6 +83,28 @@ class GolEngine:
         self._chk(N.lib.gol_snapshot(self._h, out.ctypes.data_as(N._u32p), self.wwords))
         return out
 
+    def snapshot_async(self, out: np.ndarray) -> None:
+        """Start copying the current board into `out` (as snapshot()'s
+        buffer; a page-locked one from host_buffer() keeps the call from
+        blocking) while later steps run; snapshot_wait() finishes it."""
+        if out.dtype != np.uint32 or out.shape != (self.rows, self.wwords) or not out.flags.c_contiguous:
+            raise ValueError(f"snapshot buffer must be a C-contiguous uint32 array of shape {(self.rows, self.wwords)}")
+        self._chk(N.lib.gol_snapshot_async(self._h, out.ctypes.data_as(N._u32p), self.wwords))
+        self._snap_out = out  # keep the buffer alive while the copy is in flight
+
+    def snapshot_wait(self) -> int:
+        """Finish the snapshot started by snapshot_async; returns its epoch."""
+        e = ctypes.c_uint64(0)
+        try:
+            self._chk(N.lib.gol_snapshot_wait(self._h, ctypes.byref(e)))
+        finally:
+            self._snap_out = None
+        return e.value
+
+    def host_buffer(self) -> np.ndarray:
+        """A page-locked (rows, wwords) uint32 buffer for snapshots / loads."""
+        return host_array((self.rows, self.wwords))
+
     def step(self, generations: int = 1, hashes: bool = False):
         """Advance; returns the per-generation partial hashes (uint64) if asked."""
         if hashes:
@@ -232,6 +254,31 @@ class ShardGroup:
             self.close()
         except Exception:
             pass
+
+
+class _HostBlock:
+    """Owner of one gol_host_alloc block; freed when the last array viewing
+    it is garbage-collected."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = ctypes.c_void_p()
+        N.check(N.lib.gol_host_alloc(nbytes, ctypes.byref(self.ptr)))
+
+    def __del__(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            N.lib.gol_host_free(self.ptr)
+            self.ptr = None
+
+
+def host_array(shape, dtype=np.uint32) -> np.ndarray:
+    """A numpy array over page-locked host memory (gol_host_alloc); the block
+    is freed when the array (and every view of it) is garbage-collected."""
+    dt = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dt.itemsize
+    block = _HostBlock(max(1, nbytes))
+    buf = (ctypes.c_char * max(1, nbytes)).from_address(block.ptr.value)
+    buf._gol_block = block  # array -> buf -> block
+    return np.frombuffer(buf, dtype=dt, count=int(np.prod(shape))).reshape(shape)
 
 
 def selftest(device: int = 0) -> np.ndarray:

@@ -169,6 +169,26 @@ int gol_hash(gol_ctx* ctx, uint64_t* hash_out);
  * (CellActor.scala:89, LoggerActor.scala:30-46). */
 int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words);
 
+/* Periodic snapshots without stalling the generation pipeline: the same copy
+ * as gol_snapshot, started at the current epoch and finished in the
+ * background while later gol_step calls run (LoggerActor's periodic board
+ * dump, LoggerActor.scala:30-46, fed by one CellStateMsg per cell and epoch,
+ * CellActor.scala:89).  The board is first copied on the device (one more
+ * plane of HBM, allocated on first use), then to `packed_out` on a transfer
+ * stream.  `packed_out` must stay valid and unread until gol_snapshot_wait
+ * returns; page-locked memory (gol_host_alloc) keeps the call from blocking
+ * on a staged copy.  One snapshot in flight per context (GOL_ESTATE). */
+int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words);
+
+/* Wait for the snapshot started by gol_snapshot_async; *epoch_out (may be
+ * NULL) receives the epoch the copy holds.  GOL_ESTATE if none is in flight. */
+int gol_snapshot_wait(gol_ctx* ctx, uint64_t* epoch_out);
+
+/* Page-locked host memory for snapshot / load buffers (the JVM side wraps it
+ * in a direct ByteBuffer); free with gol_host_free. */
+int gol_host_alloc(size_t bytes, void** out);
+void gol_host_free(void* p);
+
 /* State of one cell of the shard at the current epoch (0/1).  Replaces the
  * GetStateFromEpoch -> StateForEpoch exchange (CellActor.scala:71-77). */
 int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state);
