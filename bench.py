@@ -112,9 +112,12 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
     kms, launches, gens = eng.profile_read()
     eng.profile(False)
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        # every rank's own time (rank order) -> the job's time is their max
+        t = torch.zeros(world, dtype=torch.float64)
+        t[dist.get_rank()] = dt
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        timed_run.rank_times = [float(x) for x in t.tolist()]
+        dt = max(timed_run.rank_times)
     return dt, kms, launches, gens
 
 
@@ -451,6 +454,13 @@ def main():
                    "fused_hash": bool(a.hash)},
         "roofline": roof,
     }
+    if world > 1:
+        rt = timed_run.rank_times
+        out["ranks"] = {"ms_per_step": [round(x / a.steps * 1e3, 4) for x in rt],
+                        "rows": [N.shard_rows(H, r, world)[1] for r in range(world)],
+                        "gcups": [round(W * N.shard_rows(H, r, world)[1] * a.steps / x / 1e9, 2)
+                                  for r, x in enumerate(rt)],
+                        "note": "each rank's own timed window (clock stopped at its own sync); value uses the max"}
     if hashed is not None:
         out["with_state_hash"] = hashed
     if ring is not None:

@@ -49,6 +49,9 @@ def test_multirank_bench_line(tmp_path, world):
     assert d["roofline"]["bound"] == "valu"
     assert "cpu_baseline" not in d  # rank 0 at N = 1 only
     assert "note" in d["secondary"] and d["secondary"]["value"] > 0
+    rk = d["ranks"]
+    assert len(rk["ms_per_step"]) == world and sum(rk["rows"]) == 262144
+    assert abs(max(rk["ms_per_step"]) - d["ms_per_step"]) < 1e-3
     uids = set()
     H = 262144
     for r, log in enumerate(logs):
