@@ -33,7 +33,11 @@ std::string g_err;  // process-wide last error (gol_create failures)
 
 struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
+    int clk_slot = -1;  // this launch's clock-probe slot (gol_stencil.h clock_probe), or -1
 };
+
+// Clock-probe slots per context (one per profiled launch between folds).
+constexpr uint32_t kClockSlots = 4096;
 
 }  // namespace
 
@@ -93,6 +97,9 @@ struct gol_ctx {
     double prof_ms = 0.0;
     uint64_t prof_launches = 0;
     uint64_t prof_gens = 0;  // generations covered by the profiled launches
+    unsigned long long* clk_buf = nullptr;  // kClockSlots x kClockSlotWords u64 (device)
+    uint32_t clk_used = 0;                  // slots handed out since the last fold
+    double prof_clk_ms_ghz = 0.0, prof_clk_ms = 0.0;  // time-weighted probe clock
     // occupancy
     int num_cus = 0;
     std::map<int, int64_t> occupancy_cache;
@@ -176,15 +183,48 @@ void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out) {
 
 EventPair* next_event_pair(gol_ctx* ctx);
 
+// Clock one launch ran at, from its probe slot (gol_stencil.h
+// clock_probe_*): core-clock ticks over 100 MHz reference ticks, summed over
+// the launch's workgroups.
+double slot_clock_ghz(const unsigned long long* w) {
+    return w[1] ? (double)w[0] / (double)w[1] * 0.1 : 0.0;
+}
+
 int fold_profile(gol_ctx* ctx) {
+    std::vector<float> times(ctx->evs_used, 0.f);
     for (size_t i = 0; i < ctx->evs_used; ++i) {
         HIP_CHECK(ctx, hipEventSynchronize(ctx->evs[i].stop));
-        float ms = 0.f;
-        HIP_CHECK(ctx, hipEventElapsedTime(&ms, ctx->evs[i].start, ctx->evs[i].stop));
+        HIP_CHECK(ctx, hipEventElapsedTime(&times[i], ctx->evs[i].start, ctx->evs[i].stop));
+    }
+    // every probed launch has finished (its stop event fired): read the slots
+    std::vector<unsigned long long> clk;
+    if (ctx->clk_used > 0) {
+        clk.resize((size_t)ctx->clk_used * gol::kClockSlotWords);
+        HIP_CHECK(ctx, hipMemcpy(clk.data(), ctx->clk_buf, clk.size() * sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < ctx->evs_used; ++i) {
+        const float ms = times[i];
         ctx->prof_ms += ms;
         ctx->prof_launches += 1;
+        const int slot = ctx->evs[i].clk_slot;
+        if (slot >= 0 && (size_t)slot < (size_t)ctx->clk_used) {
+            const double ghz = slot_clock_ghz(clk.data() + (size_t)slot * gol::kClockSlotWords);
+            if (ghz > 0.0) {
+                ctx->prof_clk_ms_ghz += ghz * ms;
+                ctx->prof_clk_ms += ms;
+            }
+        }
+        ctx->evs[i].clk_slot = -1;
     }
     ctx->evs_used = 0;
+    if (ctx->clk_used > 0) {
+        HIP_CHECK(ctx, hipMemsetAsync(ctx->clk_buf, 0,
+                                      (size_t)ctx->clk_used * gol::kClockSlotWords * sizeof(unsigned long long),
+                                      ctx->compute));
+        HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+        ctx->clk_used = 0;
+    }
     return GOL_OK;
 }
 
@@ -451,9 +491,14 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.xcd_chunk = xcd_chunk();
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
+    p.clk = nullptr;
     if (ctx->prof && main_launch) {
         ev = next_event_pair(ctx);
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
+        if (ctx->clk_buf && ctx->clk_used < kClockSlots) {
+            ev->clk_slot = (int)ctx->clk_used++;
+            p.clk = ctx->clk_buf + (size_t)ev->clk_slot * gol::kClockSlotWords;
+        }
         HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
     }
     HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, 1, stream));
@@ -724,6 +769,7 @@ void destroy_impl(gol_ctx* c) {
     if (c->ev_snap_ready) hipEventDestroy(c->ev_snap_ready);
     if (c->ev_snap_done) hipEventDestroy(c->ev_snap_done);
     if (c->snap) hipFree(c->snap);
+    if (c->clk_buf) hipFree(c->clk_buf);
     for (auto* p : c->plane) if (p) hipFree(p);
     if (c->halo_top) hipFree(c->halo_top);
     if (c->halo_bot) hipFree(c->halo_bot);
@@ -1282,7 +1328,25 @@ int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count) {
 
 int gol_profile_enable(gol_ctx* ctx, int enable) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    const char* probe = getenv("GOL_CLOCK_PROBE");  // "0": no in-kernel clock probe (A/B)
+    if (enable && !ctx->clk_buf && !(probe && probe[0] == '0')) {
+        if (int rc = bind(ctx)) return rc;
+        const size_t bytes = (size_t)kClockSlots * gol::kClockSlotWords * sizeof(unsigned long long);
+        if (hipMalloc(&ctx->clk_buf, bytes) != hipSuccess) {
+            ctx->clk_buf = nullptr;
+            return set_err(ctx, GOL_ENOMEM, "clock-probe buffer allocation failed");
+        }
+        HIP_CHECK(ctx, hipMemset(ctx->clk_buf, 0, bytes));
+    }
     ctx->prof = enable != 0;
+    return GOL_OK;
+}
+
+int gol_profile_clock(gol_ctx* ctx, double* ghz) {
+    if (!ctx || !ghz) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (int rc = bind(ctx)) return rc;
+    if (int rc = fold_profile(ctx)) return rc;
+    *ghz = ctx->prof_clk_ms > 0.0 ? ctx->prof_clk_ms_ghz / ctx->prof_clk_ms : 0.0;
     return GOL_OK;
 }
 
@@ -1303,6 +1367,7 @@ int gol_profile_reset(gol_ctx* ctx) {
     ctx->prof_ms = 0.0;
     ctx->prof_launches = 0;
     ctx->prof_gens = 0;
+    ctx->prof_clk_ms_ghz = ctx->prof_clk_ms = 0.0;
     return GOL_OK;
 }
 

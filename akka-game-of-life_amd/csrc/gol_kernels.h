@@ -78,7 +78,10 @@ struct StepParams {
     uint32_t survive;
     int32_t variant;           // multi-generation kernel: 1 vertical-first, 2 horizontal-first
     int32_t xcd_chunk;         // consecutive blocks kept on one XCD (gol_stencil.h xcd_block; <= 1: off)
+    unsigned long long* clk;   // launch clock probe slot (kClockSlotWords u64), or null (gol_stencil.h clock_probe_*)
 };
+
+constexpr int kClockSlotWords = 2;  // summed core-clock ticks, summed 100 MHz reference ticks
 
 // Strip geometry of a launch: words covered per wave.
 int strip_words(int vec, int gens);

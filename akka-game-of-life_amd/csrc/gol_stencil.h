@@ -175,6 +175,28 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks, int chunk) {
     return g * group + (r & 7) * chunk + (r >> 3);
 }
 
+// Launch clock probe (profiling only, p.clk non-null): wave 0 of every
+// workgroup reads its CU's core-clock counter (s_memtime) and the 100 MHz
+// reference counter (s_memrealtime) when it starts and when it ends, and adds
+// both differences into the launch's slot with vector atomics.  The core
+// counters of different CUs are not aligned, so only same-wave differences
+// are used; the host divides the two sums (gol_profile_clock).
+struct ClockStart {
+    unsigned long long mt, rt;
+};
+
+__device__ __forceinline__ ClockStart clock_probe_begin(const unsigned long long* clk) {
+    if (clk == nullptr) return {0, 0};
+    return {__builtin_amdgcn_s_memtime(), __builtin_amdgcn_s_memrealtime()};
+}
+
+__device__ __forceinline__ void clock_probe_end(unsigned long long* clk, ClockStart t0) {
+    if (clk == nullptr || threadIdx.x != 0) return;
+    const unsigned long long mt = __builtin_amdgcn_s_memtime(), rt = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(clk + 0, mt - t0.mt);
+    atomicAdd(clk + 1, rt - t0.rt);
+}
+
 struct WaveTile {
     int range, strip, band;
 };
@@ -455,6 +477,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
+    const ClockStart clk0 = clock_probe_begin(p.clk);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc = 0;
 
@@ -565,6 +588,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
         if constexpr (HASH) acc = hash_lane_total(hacc, col, active);
     }
     if constexpr (HASH) hash_flush(acc, p.hash_slots, lane, wave_in_wg);
+    clock_probe_end(p.clk, clk0);
 }
 
 // --------------------------------------------------------------------------
@@ -578,6 +602,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
+    const ClockStart clk0 = clock_probe_begin(p.clk);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
@@ -692,6 +717,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
 #pragma unroll
         for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
     }
+    clock_probe_end(p.clk, clk0);
 }
 
 // --------------------------------------------------------------------------
@@ -817,6 +843,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
+    const ClockStart clk0 = clock_probe_begin(p.clk);
     const int rg = tile.range, strip = tile.strip, bandi = tile.band;
     unsigned long long acc[G];
 #pragma unroll
@@ -973,6 +1000,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 #pragma unroll
         for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
     }
+    clock_probe_end(p.clk, clk0);
 }
 
 // The horizontal-first kernel keeps three planes per ring row: at 16-byte

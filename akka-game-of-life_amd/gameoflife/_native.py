@@ -77,6 +77,7 @@ _SIGNATURES = {
     "gol_sync": (_c.c_int, [_vp]),
     "gol_hash": (_c.c_int, [_vp, _u64p]),
     "gol_snapshot": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_profile_clock": (_c.c_int, [_vp, ctypes.POINTER(_c.c_double)]),
     "gol_snapshot_async": (_c.c_int, [_vp, _u32p, _c.c_int64]),
     "gol_snapshot_wait": (_c.c_int, [_vp, _u64p]),
     "gol_host_alloc": (_c.c_int, [_c.c_size_t, ctypes.POINTER(_vp)]),

@@ -184,6 +184,13 @@ class GolEngine:
     def profile_reset(self) -> None:
         self._chk(N.lib.gol_profile_reset(self._h))
 
+    def profile_clock(self) -> float:
+        """GHz the GPU held during the profiled launches since the reset
+        (in-kernel clock probe, gol_profile_clock); 0.0 if none."""
+        g = ctypes.c_double(0)
+        self._chk(N.lib.gol_profile_clock(self._h, ctypes.byref(g)))
+        return g.value
+
     def occupancy(self, gens_per_pass: int) -> tuple[int, int]:
         """(resident waves per CU, strip width in words) of a G-generation pass."""
         w, s = ctypes.c_int32(0), ctypes.c_int32(0)

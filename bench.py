@@ -21,7 +21,9 @@ HBM -- temporal blocking fuses 6-8 generations per pass over the plane.  So:
   * roofline.bound = "valu": achieved = cell-updates per second of that launch
     (cells x generations per launch / its mean HIP-event duration), peak = the
     VALU-issue ceiling of the kernel's loop mix at the clock the chip held
-    during those launches (PMC GRBM_GUI_ACTIVE, profiles/pmc_launch.json);
+    during those launches (an in-kernel probe of the timed launches,
+    gol_profile_clock; PMC GRBM_GUI_ACTIVE from profiles/pmc_launch.json
+    beside it as clock_pmc_ghz);
   * roofline.traffic = PMC HBM bytes per launch, and roofline.hbm the physical
     HBM bandwidth that implies against the 8 TB/s spec;
   * roofline.hbm_effective = SURVEY.md section 8(d)'s 2 bits per cell-update,
@@ -110,6 +112,7 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
     dt = time.perf_counter() - t0
     barrier(dist, world)
     kms, launches, gens = eng.profile_read()
+    clock = eng.profile_clock()  # GHz the timed launches ran at (in-kernel probe)
     eng.profile(False)
     if world > 1:
         # every rank's own time (rank order) -> the job's time is their max
@@ -118,7 +121,7 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         timed_run.rank_times = [float(x) for x in t.tolist()]
         dt = max(timed_run.rank_times)
-    return dt, kms, launches, gens
+    return dt, kms, launches, gens, clock
 
 
 def cpu_model():
@@ -199,8 +202,10 @@ def compact_plan(plan):
     return " + ".join(f"{n} x {g}" for n, g in runs)
 
 
-def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False):
-    """Roofline of the dominant kernel (see the module docstring)."""
+def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None):
+    """Roofline of the dominant kernel (see the module docstring).  `clock`:
+    GHz the timed launches ran at, from the in-kernel probe
+    (gol_profile_clock); the PMC table's clock is the fallback."""
     if not launches:
         return None
     avg_s = kms / 1e3 / launches
@@ -221,14 +226,19 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
             r["traffic_source"] = "profiles/pmc_launch.json " + ", ".join(pmc["keys"])
         return r
     mix = VALU_MIX_HASH if hashed else VALU_MIX
-    clock = pmc["clock_ghz"] if pmc else CLOCK_MAX_GHZ
+    live = bool(clock)
+    if not live:
+        clock = pmc["clock_ghz"] if pmc else CLOCK_MAX_GHZ
     peak, cycles = valu_peak_gcups(mix, clock)
     peak_max, _ = valu_peak_gcups(mix, CLOCK_MAX_GHZ)
     r = {"bound": "valu", "achieved": round(gcups, 1), "peak": round(peak, 1), "unit": "GCUPS",
          "frac": round(gcups / peak, 4), "traffic": round(pmc["hbm_bytes"]) if pmc else None,
          "clock_ghz": round(clock, 3),
-         "clock_source": ("PMC GRBM_GUI_ACTIVE / 8 / launch time, time-weighted over the plan "
+         "clock_source": ("in-kernel probe of these timed launches: every workgroup's core-clock (s_memtime) "
+                          "and 100 MHz reference (s_memrealtime) ticks, summed (gol_profile_clock)") if live else
+                         ("PMC GRBM_GUI_ACTIVE / 8 / launch time, time-weighted over the plan "
                           "(profiles/pmc_launch.json)") if pmc else "max clock (no PMC entry for this plan)",
+         "clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None,
          "frac_at_max_clock": round(gcups / peak_max, 4),
          "valu": {"instructions_per_word_generation": {k: n for k, (n, _) in mix.items()},
                   "cycles_per_word_generation": round(cycles, 2),
@@ -291,10 +301,10 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
         e2.seed(0x5EED)
         n_s, w_s = max(a.steps, 102), max(a.warmup, 12)
-        dt_s, _, _, _ = timed_run(e2, torch, dist, 1, n_s, w_s, a.hash)
+        dt_s, _, _, _, _ = timed_run(e2, torch, dist, 1, n_s, w_s, a.hash)
         settle(e2, 50.0, a.hash, 64)
         n2 = max(a.steps, 1024)
-        dt2, kms2, l2, g2 = timed_run(e2, torch, dist, 1, n2, 0, a.hash)
+        dt2, kms2, l2, g2, c2 = timed_run(e2, torch, dist, 1, n2, 0, a.hash)
         plan2 = e2.pass_plan(n2, hashes=a.hash)
         # the same board one generation per HBM pass: the pure bandwidth case
         # (north_star: >= 70 % of peak HBM bandwidth at 65536^2)
@@ -302,10 +312,10 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.seed(0x5EED)
         settle(e2, 50.0, a.hash, 16)
         n1 = max(a.steps, 256)
-        dt1, kms1, l1, g1 = timed_run(e2, torch, dist, 1, n1, 0, a.hash)
+        dt1, kms1, l1, g1, c1 = timed_run(e2, torch, dist, 1, n1, 0, a.hash)
     shape = f"{S}x{S}"
-    r2 = roofline(kms2, l2, g2, S * S, plan2, shape, "N1", a.hash)
-    r1 = roofline(kms1, l1, g1, S * S, [1] * n1, shape, "N1", a.hash)
+    r2 = roofline(kms2, l2, g2, S * S, plan2, shape, "N1", a.hash, c2)
+    r1 = roofline(kms1, l1, g1, S * S, [1] * n1, shape, "N1", a.hash, c1)
     out.update({
         "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": "50 ms settled",
         "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2,
@@ -333,7 +343,7 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     eng.comm_init(N.unique_id(), 0, 1)
     eng.seed(0x5EED)
     settle(eng, 50.0, False, 12)
-    dt, kms, launches, gcov = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
+    dt, kms, launches, gcov, _ = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
     out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
                                     "warmup": warm, "ms_per_step": round(dt / a.steps * 1e3, 4),
                                     "pass_plan": eng.pass_plan(min(a.steps, 1024))}
@@ -348,7 +358,7 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
         if not a.no_secondary:
             secondary_run(GolEngine, torch, dist, a, local)
         e8.seed(0x5EED)
-        dtf, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        dtf, _, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         out["per_rank_shard_driver_window"] = {
             "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dtf / 1e9, 2),
             "unit": "GCUPS", "warmup": a.warmup, "ms_per_step": round(dtf / a.steps * 1e3, 4),
@@ -357,13 +367,13 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
                     "run can reach before any xGMI cost"}
         e8.seed(0x5EED)
         settle(e8, 50.0, False, 12)
-        dt8, kms8, l8, g8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        dt8, kms8, l8, g8, c8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         plan8 = e8.pass_plan(min(a.steps, 1024))
     out["per_rank_shard_self_ring"] = {
         "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
         "unit": "GCUPS", "warmup": warm, "ms_per_step": round(dt8 / a.steps * 1e3, 4), "pass_plan": plan8,
         "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
-                                    f"{W}x{rows8}", "ring")}
+                                    f"{W}x{rows8}", "ring", False, c8)}
     return out
 
 
@@ -405,7 +415,7 @@ def main():
             secondary["note"] = f"measured on rank {rank}'s GPU; each of the {world} ranks ran it on its own GPU"
     eng.seed(0x5EED)
 
-    dt, kms, launches, gcov = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    dt, kms, launches, gcov, clk = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
     eng_info = {g: eng.occupancy(g) for g in range(1, 13)}
     plan = eng.pass_plan(min(a.steps, 1024), hashes=a.hash)
     value = W * H * a.steps / dt / 1e9
@@ -414,19 +424,20 @@ def main():
         # the same workload with the fused per-generation state hash (the
         # parity contract's output: one u64 per generation),
         # continuing from the board the timed run left
-        dth, kmsh, lh, gh = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
+        dth, kmsh, lh, gh, ch = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
         hplan = eng.pass_plan(min(a.steps, 1024), hashes=True)
         vh = W * H * a.steps / dth / 1e9
         hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
                   "frac_of_unhashed": round(vh / value, 4), "pass_plan": hplan,
-                  "roofline": roofline(kmsh, lh, gh, W * H, hplan, f"{W}x{H}", "N1", True)}
+                  "roofline": roofline(kmsh, lh, gh, W * H, hplan, f"{W}x{H}", "N1", True, ch)}
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
     G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
     if world == 1:
-        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash)
+        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash, clk)
     else:
-        roof = roofline(kms, launches, gcov, W * max(rows - round(2 * G), 0), plan, f"{W}x{rows}", "ring", a.hash)
+        roof = roofline(kms, launches, gcov, W * max(rows - round(2 * G), 0), plan, f"{W}x{rows}", "ring", a.hash,
+                        clk)
     if roof is not None:
         roof["kernel"] = kernel_label(eng_info, plan)
     ring = None

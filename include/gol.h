@@ -246,6 +246,10 @@ void gol_group_destroy(gol_group* group);
 int gol_profile_enable(gol_ctx* ctx, int enable);
 int gol_profile_read(gol_ctx* ctx, double* total_ms, uint64_t* launches, uint64_t* generations);
 int gol_profile_reset(gol_ctx* ctx);
+/* Clock (GHz) the GPU held during the profiled launches since the last
+ * reset, time-weighted: each launch's workgroups read their XCD's core-clock
+ * and 100 MHz reference counters at start and end (0 if none recorded). */
+int gol_profile_clock(gol_ctx* ctx, double* ghz);
 
 /* Tuning knobs (results never depend on them); 0 selects the automatic
  * choice, which is also the default of a new context:

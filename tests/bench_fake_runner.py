@@ -73,6 +73,9 @@ class FakeEngine:
     def profile_read(self):
         return self.ms, self.launches, self.gens
 
+    def profile_clock(self):
+        return 2.0 if self.launches else 0.0
+
     def occupancy(self, g):
         return (12 if g > 8 else 16), 124
 

@@ -54,3 +54,16 @@ def test_hashed_mix_adds_the_multiply_add():
 def test_compact_plan_keeps_json_short():
     assert bench.compact_plan([1] * 256) == "256 x 1"
     assert bench.compact_plan([12] * 7 + [9, 9]) == "7 x 12 + 2 x 9"
+
+
+def test_live_probe_clock_takes_precedence(monkeypatch):
+    """The clock measured inside the timed launches (gol_profile_clock) prices
+    the VALU ceiling; the PMC table's clock stays beside it."""
+    ent = {"launch_ms": 4.0, "hbm_bytes": 18e9, "clock_ghz": 2.2, "valu_per_word_gen": 12.0,
+           "generations_per_launch": 12}
+    _table(monkeypatch, {"262144x262144/N1/G12/h0": ent})
+    r = bench.roofline(kms=12.0, launches=2, gens_covered=24, cells=262144 * 262144, plan=[12, 12],
+                       shape="262144x262144", mode="N1", clock=1.9)
+    assert r["clock_ghz"] == 1.9 and "probe" in r["clock_source"] and r["clock_pmc_ghz"] == 2.2
+    peak, _ = bench.valu_peak_gcups(bench.VALU_MIX, 1.9)
+    assert abs(r["peak"] - round(peak, 1)) < 0.2 and r["traffic"] == 18e9

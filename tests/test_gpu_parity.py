@@ -365,3 +365,28 @@ def test_replay_light_cone(gpu, W, topology, row0, rows, d):
         assert (e.snapshot() == cur[row0:row0 + rows]).all()
         with pytest.raises(Exception):
             e.replay(2, up[:1], dn[:1])  # light-cone rows of the wrong depth
+
+
+def test_profile_clock_probe(gpu):
+    """gol_profile_clock: the in-kernel probe (every workgroup's XCD core-clock
+    and 100 MHz reference counters at start and end) yields the clock of the
+    profiled launches -- plausible for an MI355X (its max is 2.4 GHz) -- and
+    the probe leaves the results bit-exact."""
+    W, H = 32 * 1024, 1024
+    board = O.seed_packed(W, H, 0x5EED)
+    with engine(W, H) as e:
+        e.seed(0x5EED)
+        e.profile(True)
+        e.profile_reset()
+        assert e.profile_clock() == 0.0
+        got = e.step(40, hashes=True)
+        ms, n, g = e.profile_read()
+        clk = e.profile_clock()
+        assert n > 0 and g == 40 and 0.3 < clk < 2.6, clk
+        e.profile_reset()
+        assert e.profile_clock() == 0.0
+        e.profile(False)
+        final = e.snapshot()
+    want_board, want = O.run_packed(board, W, 40)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(final, want_board)
