@@ -33,7 +33,7 @@ std::string g_err;  // process-wide last error (gol_create failures)
 
 struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
-    int clk_slot = -1;  // this launch's clock-probe slot (gol_stencil.h clock_probe), or -1
+    int clk_slot = -1;  // this launch's clock-probe slot (gol_stencil.h clock_probe_*), or -1
 };
 
 // Clock-probe slots per context (one per profiled launch between folds).
@@ -1181,10 +1181,10 @@ int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_wo
             ctx->snap = nullptr;
             return set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes for the snapshot buffer failed", bytes);
         }
-        HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->xfer, hipStreamNonBlocking));
-        HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_ready, hipEventDisableTiming));
-        HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_done, hipEventDisableTiming));
     }
+    if (!ctx->xfer) HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->xfer, hipStreamNonBlocking));
+    if (!ctx->ev_snap_ready) HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_ready, hipEventDisableTiming));
+    if (!ctx->ev_snap_done) HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_done, hipEventDisableTiming));
     const uint32_t* src = ctx->plane[ctx->cur];
     if (ctx->pairs)
         HIP_CHECK(ctx, gol::launch_convert(src, ctx->snap, ctx->pitch, ctx->wwords, (int32_t)ctx->rows, false,
