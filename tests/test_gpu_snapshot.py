@@ -18,6 +18,7 @@ def _want(board, W, gens, topo=O.TORUS, rule=O.LIFE):
 
 
 @pytest.mark.parametrize("W,H,topology", [(32 * 512, 300, "torus"),     # pair layout
+                                          (32 * 100, 50, "torus"),      # pair layout, pitch 128 != 100 words
                                           (32 * 301, 77, "torus"),      # odd words: row-major torus
                                           (32 * 40 + 13, 61, "ref-clipped")])
 def test_async_snapshot_overlaps_later_steps(gpu, W, H, topology):
