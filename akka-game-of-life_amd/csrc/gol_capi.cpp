@@ -37,7 +37,7 @@ struct EventPair {
 };
 
 // Clock-probe slots per context (one per profiled launch between folds).
-constexpr uint32_t kClockSlots = 4096;
+constexpr uint32_t kClockSlots = 1024;  // 4 KiB each
 
 }  // namespace
 
@@ -187,7 +187,12 @@ EventPair* next_event_pair(gol_ctx* ctx);
 // clock_probe_*): core-clock ticks over 100 MHz reference ticks, summed over
 // the launch's workgroups.
 double slot_clock_ghz(const unsigned long long* w) {
-    return w[1] ? (double)w[0] / (double)w[1] * 0.1 : 0.0;
+    unsigned long long mt = 0, rt = 0;
+    for (int k = 0; k < gol::kClockSubSlots; ++k) {
+        mt += w[k * gol::kClockSubWords + 0];
+        rt += w[k * gol::kClockSubWords + 1];
+    }
+    return rt ? (double)mt / (double)rt * 0.1 : 0.0;
 }
 
 int fold_profile(gol_ctx* ctx) {

@@ -81,7 +81,12 @@ struct StepParams {
     unsigned long long* clk;   // launch clock probe slot (kClockSlotWords u64), or null (gol_stencil.h clock_probe_*)
 };
 
-constexpr int kClockSlotWords = 2;  // summed core-clock ticks, summed 100 MHz reference ticks
+// Per launch: kClockSubSlots sub-slots one 64-B line apart, each summing
+// core-clock ticks and 100 MHz reference ticks of the sampled workgroups.
+constexpr int kClockSubSlots = 64;
+constexpr int kClockSubWords = 8;
+constexpr int kClockSampleEvery = 4;
+constexpr int kClockSlotWords = kClockSubSlots * kClockSubWords;
 
 // Strip geometry of a launch: words covered per wave.
 int strip_words(int vec, int gens);

@@ -178,7 +178,8 @@ __device__ __forceinline__ int xcd_block(int b, int nblocks, int chunk) {
 // Launch clock probe (profiling only, p.clk non-null): wave 0 of every
 // workgroup reads its CU's core-clock counter (s_memtime) and the 100 MHz
 // reference counter (s_memrealtime) when it starts and when it ends, and adds
-// both differences into the launch's slot with vector atomics.  The core
+// both differences into the launch's slot with vector atomics (a sample of
+// the workgroups, spread over sub-slots).  The core
 // counters of different CUs are not aligned, so only same-wave differences
 // are used; the host divides the two sums (gol_profile_clock).
 struct ClockStart {
@@ -191,10 +192,15 @@ __device__ __forceinline__ ClockStart clock_probe_begin(const unsigned long long
 }
 
 __device__ __forceinline__ void clock_probe_end(unsigned long long* clk, ClockStart t0) {
-    if (clk == nullptr || threadIdx.x != 0) return;
+    // One workgroup in kClockSampleEvery reports, into one of kClockSubSlots
+    // cache lines: a single-generation launch has ~10^5 workgroups, and
+    // atomics on one address serialise (every workgroup on two addresses
+    // made the 65536^2 single-generation pass 4x slower).
+    if (clk == nullptr || threadIdx.x != 0 || blockIdx.x % kClockSampleEvery != 0) return;
     const unsigned long long mt = __builtin_amdgcn_s_memtime(), rt = __builtin_amdgcn_s_memrealtime();
-    atomicAdd(clk + 0, mt - t0.mt);
-    atomicAdd(clk + 1, rt - t0.rt);
+    unsigned long long* sub = clk + (blockIdx.x / kClockSampleEvery % kClockSubSlots) * kClockSubWords;
+    atomicAdd(sub + 0, mt - t0.mt);
+    atomicAdd(sub + 1, rt - t0.rt);
 }
 
 struct WaveTile {
