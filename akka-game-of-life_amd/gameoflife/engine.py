@@ -272,9 +272,12 @@ class _HostBlock:
         N.check(N.lib.gol_host_alloc(nbytes, ctypes.byref(self.ptr)))
 
     def __del__(self):
-        if getattr(self, "ptr", None) is not None and self.ptr.value:
-            N.lib.gol_host_free(self.ptr)
-            self.ptr = None
+        try:
+            if getattr(self, "ptr", None) is not None and self.ptr.value:
+                N.lib.gol_host_free(self.ptr)
+                self.ptr = None
+        except Exception:  # interpreter shutdown: the library may be gone already
+            pass
 
 
 def host_array(shape, dtype=np.uint32) -> np.ndarray:
