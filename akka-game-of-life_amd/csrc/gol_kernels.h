@@ -7,7 +7,10 @@
 namespace gol {
 
 constexpr int kWaveLanes = 64;   // CDNA wavefront
-constexpr int kWavesPerWG = 4;   // 256-thread workgroups
+#ifndef GOL_WAVES_PER_WG
+#define GOL_WAVES_PER_WG 4
+#endif
+constexpr int kWavesPerWG = GOL_WAVES_PER_WG;  // waves per workgroup (256-thread workgroups)
 constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line each)
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
