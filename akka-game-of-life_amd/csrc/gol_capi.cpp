@@ -1278,6 +1278,21 @@ int gol_checkpoint(gol_ctx* ctx, void* host_out, size_t bytes) {
     return gol_snapshot(ctx, reinterpret_cast<uint32_t*>(static_cast<char*>(host_out) + sizeof h), ctx->wwords);
 }
 
+int gol_checkpoint_async(gol_ctx* ctx, void* host_out, size_t bytes) {
+    size_t need = 0;
+    if (!ctx || !host_out) return set_err(ctx, GOL_EINVAL, "null argument");
+    gol_checkpoint_bytes(ctx, &need);
+    if (bytes < need) return set_err(ctx, GOL_EINVAL, "checkpoint buffer too small (%zu < %zu)", bytes, need);
+    if (ctx->snap_pending) return set_err(ctx, GOL_ESTATE, "a snapshot is in flight: call gol_snapshot_wait first");
+    CkptHeader h{};
+    memcpy(h.magic, "GOLCKPT1", 8);
+    h.width = ctx->width; h.height = ctx->height; h.row0 = ctx->row0; h.rows = ctx->rows;
+    h.wwords = ctx->wwords; h.epoch = ctx->epoch; h.topology = ctx->topology;
+    h.birth = ctx->birth; h.survive = ctx->survive;
+    memcpy(host_out, &h, sizeof h);
+    return gol_snapshot_async(ctx, reinterpret_cast<uint32_t*>(static_cast<char*>(host_out) + sizeof h), ctx->wwords);
+}
+
 int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes) {
     if (!ctx || !host_in) return set_err(ctx, GOL_EINVAL, "null argument");
     if (bytes < sizeof(CkptHeader)) return set_err(ctx, GOL_EINVAL, "checkpoint truncated");

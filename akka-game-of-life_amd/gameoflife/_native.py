@@ -79,6 +79,7 @@ _SIGNATURES = {
     "gol_snapshot": (_c.c_int, [_vp, _u32p, _c.c_int64]),
     "gol_profile_clock": (_c.c_int, [_vp, ctypes.POINTER(_c.c_double)]),
     "gol_snapshot_async": (_c.c_int, [_vp, _u32p, _c.c_int64]),
+    "gol_checkpoint_async": (_c.c_int, [_vp, _vp, _c.c_size_t]),
     "gol_snapshot_wait": (_c.c_int, [_vp, _u64p]),
     "gol_host_alloc": (_c.c_int, [_c.c_size_t, ctypes.POINTER(_vp)]),
     "gol_host_free": (None, [_vp]),

@@ -140,9 +140,24 @@ class GolEngine:
         self._chk(N.lib.gol_checkpoint(self._h, buf, n.value))
         return buf.raw
 
-    def restore(self, blob: bytes) -> None:
-        buf = ctypes.create_string_buffer(blob, len(blob))
-        self._chk(N.lib.gol_restore(self._h, buf, len(blob)))
+    def checkpoint_bytes(self) -> int:
+        n = ctypes.c_size_t(0)
+        self._chk(N.lib.gol_checkpoint_bytes(self._h, ctypes.byref(n)))
+        return n.value
+
+    def checkpoint_async(self, out: np.ndarray) -> None:
+        """Start a checkpoint into `out` (uint8, checkpoint_bytes() long; a
+        page-locked one from host_array keeps the call from blocking); finish
+        it with snapshot_wait()."""
+        if out.dtype != np.uint8 or out.size < self.checkpoint_bytes() or not out.flags.c_contiguous:
+            raise ValueError("checkpoint buffer must be a C-contiguous uint8 array of checkpoint_bytes()")
+        self._chk(N.lib.gol_checkpoint_async(self._h, out.ctypes.data_as(ctypes.c_void_p), out.size))
+        self._snap_out = out
+
+    def restore(self, blob) -> None:
+        """Restore a checkpoint (bytes, or any buffer such as a uint8 array)."""
+        arr = np.frombuffer(blob, dtype=np.uint8)
+        self._chk(N.lib.gol_restore(self._h, arr.ctypes.data_as(ctypes.c_void_p), arr.size))
 
     # -- multi-GPU -----------------------------------------------------------
     def comm_init(self, uid: bytes, rank: int, nranks: int) -> None:

@@ -32,7 +32,7 @@ import os
 import numpy as np
 
 from .elastic import blob_rows, light_cone_from
-from .engine import GolEngine, ShardGroup
+from .engine import GolEngine, ShardGroup, host_array
 from .shard import shard_rows_py
 
 
@@ -40,13 +40,21 @@ class ShardedSimulation:
     def __init__(self, width: int, height: int, nshards: int, devices: list[int] | None = None,
                  topology: str = "torus", rule="life", seed: int = 0x5EED,
                  checkpoint_every: int = 10, checkpoint_dir: str | None = None,
-                 gens_per_pass: int = 0):
+                 gens_per_pass: int = 0, async_checkpoints: bool = False):
         self.width, self.height, self.n = width, height, nshards
         self.devices = list(devices) if devices else [0]
         self.topology, self.rule = topology, rule
         self.checkpoint_every = checkpoint_every
         self.checkpoint_dir = checkpoint_dir
         self.gens_per_pass = gens_per_pass
+        # async_checkpoints: each checkpoint is taken in the background
+        # (gol_checkpoint_async into page-locked buffers, two sets) while the
+        # next generations run, and becomes the recovery point when it has
+        # landed (the next checkpoint, a loss, a snapshot or close)
+        self.async_checkpoints = async_checkpoints
+        self._ckpt_bufs: list[list] = [[], []]
+        self._ckpt_set = 0
+        self._pending_epoch: int | None = None
         self.placement = [self.devices[k % len(self.devices)] for k in range(nshards)]
         self.shards: list[GolEngine | None] = [self._make(k, self.placement[k]) for k in range(nshards)]
         for s in self.shards:
@@ -68,8 +76,31 @@ class ShardedSimulation:
 
     # ----------------------------------------------------------- checkpoints
     def checkpoint(self) -> None:
-        self.ckpt = [s.checkpoint() for s in self.shards]
-        self.ckpt_epoch = self.epoch
+        if self.async_checkpoints:
+            self._finish_checkpoint()
+            bufs = self._ckpt_bufs[self._ckpt_set]
+            if not bufs:
+                bufs.extend(host_array((s.checkpoint_bytes(),), np.uint8) for s in self.shards)
+            for s, b in zip(self.shards, bufs):
+                s.checkpoint_async(b)
+            self._pending_epoch = self.epoch
+            return
+        self._commit_checkpoint([s.checkpoint() for s in self.shards], self.epoch)
+
+    def _finish_checkpoint(self) -> None:
+        """Wait for a background checkpoint and make it the recovery point."""
+        if self._pending_epoch is None:
+            return
+        for s in self.shards:
+            s.snapshot_wait()
+        blobs = self._ckpt_bufs[self._ckpt_set]
+        self._ckpt_set ^= 1  # the next one goes to the other set; this one stays valid
+        epoch, self._pending_epoch = self._pending_epoch, None
+        self._commit_checkpoint(list(blobs), epoch)
+
+    def _commit_checkpoint(self, blobs: list, epoch: int) -> None:
+        self.ckpt = blobs
+        self.ckpt_epoch = epoch
         if self.checkpoint_dir:
             os.makedirs(self.checkpoint_dir, exist_ok=True)
             for k, blob in enumerate(self.ckpt):
@@ -77,7 +108,7 @@ class ShardedSimulation:
                 with open(tmp, "wb") as f:
                     f.write(blob)
                 os.replace(tmp, os.path.join(self.checkpoint_dir, f"shard{k}.ckpt"))
-        self.events.append(f"checkpoint@{self.epoch}")
+        self.events.append(f"checkpoint@{epoch}")
 
     # ------------------------------------------------------------------ run
     def step(self, generations: int) -> list[int]:
@@ -101,6 +132,7 @@ class ShardedSimulation:
     # ---------------------------------------------------------------- faults
     def kill(self, k: int) -> None:
         """Lose shard k (its context and device memory are gone)."""
+        self._finish_checkpoint()
         self.shards[k].close()            # the group now has a hole (gol_group_step -> GOL_ESTATE)
         self.shards[k] = None
         self.group.close()
@@ -170,9 +202,12 @@ class ShardedSimulation:
         return out
 
     def snapshot(self) -> np.ndarray:
+        self._finish_checkpoint()
         return np.vstack([s.snapshot() for s in self.shards])
 
     def close(self) -> None:
+        if all(s is not None for s in self.shards):
+            self._finish_checkpoint()
         if self.group is not None:
             self.group.close()
         for s in self.shards:

@@ -200,6 +200,12 @@ int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state);
  * (BoardCreator.scala:138-154). */
 int gol_checkpoint_bytes(const gol_ctx* ctx, size_t* bytes);
 int gol_checkpoint(gol_ctx* ctx, void* host_out, size_t bytes);
+
+/* gol_checkpoint in the background (the periodic checkpoint of the fault
+ * path overlapping the generations after it): the header is written now, the
+ * rows follow as with gol_snapshot_async; finish with gol_snapshot_wait.
+ * GOL_ESTATE while a snapshot or checkpoint is in flight. */
+int gol_checkpoint_async(gol_ctx* ctx, void* host_out, size_t bytes);
 int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes);
 
 /* Multi-GPU: RCCL communicator over the ring of row-block shards.  Replaces

@@ -143,3 +143,26 @@ def test_recurring_crashes_light_cone(gpu, topology):
     final, want = O.run_packed(O.seed_packed(W, H, 0x5EED), W, gens, topo, O.LIFE)
     assert got == [int(x) for x in want]
     assert (board == final).all()
+
+
+def test_recurring_crashes_async_checkpoints(gpu):
+    """The same recurring-crash schedule with the checkpoints taken in the
+    background (gol_checkpoint_async, two page-locked buffer sets): each loss
+    recovers from the last checkpoint that has landed, and every hash equals
+    the uninterrupted oracle run."""
+    from gameoflife import _native as N
+    from gameoflife.board import SimulationParams, crash_schedule
+    from gameoflife.fault import ShardedSimulation
+    W, H, gens = 32 * 100, 77, 60
+    p = SimulationParams(start_delay_ms=0, tick_ms=100, first_error_after_ms=500, error_every_ms=1100,
+                         max_number_of_crashes=5)
+    crashes = crash_schedule(p, gens, seed=11)
+    sim = ShardedSimulation(W, H, 8, list(range(N.device_count())), checkpoint_every=12, async_checkpoints=True)
+    got = sim.run(gens, crashes)
+    board = sim.snapshot()
+    assert sum(e.startswith("respawn") for e in sim.events) == 5
+    assert sum(e.startswith("checkpoint@") for e in sim.events) >= 5
+    sim.close()
+    final, want = O.run_packed(O.seed_packed(W, H, 0x5EED), W, gens, O.TORUS, O.LIFE)
+    assert got == [int(x) for x in want]
+    assert (board == final).all()
