@@ -133,12 +133,14 @@ class GolEngine:
         self._chk(N.lib.gol_get_cell(self._h, x, y, ctypes.byref(s)))
         return bool(s.value)
 
-    def checkpoint(self) -> bytes:
-        n = ctypes.c_size_t(0)
-        self._chk(N.lib.gol_checkpoint_bytes(self._h, ctypes.byref(n)))
-        buf = ctypes.create_string_buffer(n.value)
-        self._chk(N.lib.gol_checkpoint(self._h, buf, n.value))
-        return buf.raw
+    def checkpoint(self) -> np.ndarray:
+        """gol_checkpoint into a new uint8 array (a bytes-like buffer: file
+        writes, parse_checkpoint and restore take it as is).  No zero-fill and
+        no bytes copy: at 0.5 GiB per shard that was ~0.3 s per checkpoint."""
+        n = self.checkpoint_bytes()
+        out = np.empty(n, dtype=np.uint8)
+        self._chk(N.lib.gol_checkpoint(self._h, out.ctypes.data_as(ctypes.c_void_p), n))
+        return out
 
     def checkpoint_bytes(self) -> int:
         n = ctypes.c_size_t(0)
