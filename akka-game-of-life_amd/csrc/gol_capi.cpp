@@ -123,17 +123,54 @@ int set_err(gol_ctx* ctx, int code, const char* fmt, ...) {
     return code;
 }
 
-#define HIP_CHECK(ctx, expr)                                                                      \
-    do {                                                                                          \
-        hipError_t e_ = (expr);                                                                   \
-        if (e_ != hipSuccess)                                                                     \
-            return set_err((ctx), GOL_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
-                           __FILE__, __LINE__);                                                   \
+// HIP status discipline: a failing HIP call also
+// leaves its status pending on the calling thread (hipGetLastError).  A
+// failure libgol reports through its own return code is taken off the
+// thread here, so no later call -- ours or the caller's -- inherits it.
+int hip_fail(gol_ctx* ctx, hipError_t e, const char* expr, const char* file, int line) {
+    (void)hipGetLastError();
+    return set_err(ctx, GOL_EHIP, "%s failed: %s (%s:%d)", expr, hipGetErrorString(e), file, line);
+}
+
+#define HIP_CHECK(ctx, expr)                                                   \
+    do {                                                                       \
+        hipError_t e_ = (expr);                                                \
+        if (e_ != hipSuccess) return hip_fail((ctx), e_, #expr, __FILE__, __LINE__); \
     } while (0)
+
+// A status whose failure only gets logged (teardown, best-effort calls):
+// reported on stderr and taken off the thread.
+void hip_note(hipError_t e, const char* what) {
+    if (e == hipSuccess) return;
+    (void)hipGetLastError();
+    fprintf(stderr, "libgol: %s: %s (%d)\n", what, hipGetErrorString(e), (int)e);
+}
+
+// RCCL runs HIP calls of its own on the calling thread and does not take the
+// statuses it discards off the thread.  After every RCCL call libgol makes,
+// such a leftover is taken here -- where it arose -- counted, and logged once
+// per (call, status) pair, so it can neither be pinned on a later launch
+// nor reach the caller.  gol_diag_absorbed reports the count.
+std::mutex g_absorb_mu;
+uint64_t g_absorbed = 0;
+std::string g_absorbed_last;
+std::map<std::string, int> g_absorb_seen;
+
+void absorb_rccl_status(const char* call) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return;
+    char msg[256];
+    snprintf(msg, sizeof msg, "%s left HIP status %s (%d) on the calling thread", call, hipGetErrorString(e), (int)e);
+    std::lock_guard<std::mutex> lk(g_absorb_mu);
+    ++g_absorbed;
+    g_absorbed_last = msg;
+    if (g_absorb_seen[msg]++ == 0) fprintf(stderr, "libgol: %s (absorbed)\n", msg);
+}
 
 #define NCCL_CHECK(ctx, expr)                                                                       \
     do {                                                                                            \
         ncclResult_t r_ = (expr);                                                                   \
+        absorb_rccl_status(#expr);                                                                  \
         if (r_ != ncclSuccess)                                                                      \
             return set_err((ctx), GOL_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
                            __FILE__, __LINE__);                                                     \
@@ -240,8 +277,11 @@ EventPair* next_event_pair(gol_ctx* ctx) {
             if (fold_profile(ctx) != GOL_OK) return nullptr;
         } else {
             EventPair e;
-            if (hipEventCreate(&e.start) != hipSuccess || hipEventCreate(&e.stop) != hipSuccess)
+            if (hipEventCreate(&e.start) != hipSuccess || hipEventCreate(&e.stop) != hipSuccess) {
+                (void)hipGetLastError();  // reported by the caller as GOL_EHIP
+                if (e.start) hip_note(hipEventDestroy(e.start), "hipEventDestroy");
                 return nullptr;
+            }
             ctx->evs.push_back(e);
         }
     }
@@ -624,8 +664,8 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
     const int n = (int)g->shards.size();
     for (gol_ctx* s : g->shards) {
         if (int rc = bind(s)) return group_fail(g, s, rc);
-        if (hipEventRecord(s->ev_ready, s->compute) != hipSuccess)
-            return group_fail(g, s, set_err(s, GOL_EHIP, "hipEventRecord failed"));
+        if (hipError_t e = hipEventRecord(s->ev_ready, s->compute))
+            return group_fail(g, s, hip_fail(s, e, "hipEventRecord", __FILE__, __LINE__));
     }
     for (int k = 0; k < n; ++k) {
         gol_ctx* s = g->shards[k];
@@ -643,8 +683,7 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
         if (e == hipSuccess && has_down)
             e = hipMemcpyPeerAsync(s->halo_bot, s->device, dn->plane[dn->cur], dn->device, bytes, s->comm);
         if (e == hipSuccess) e = hipEventRecord(s->ev_halo, s->comm);
-        if (e != hipSuccess)
-            return group_fail(g, s, set_err(s, GOL_EHIP, "halo pull failed: %s", hipGetErrorString(e)));
+        if (e != hipSuccess) return group_fail(g, s, hip_fail(s, e, "halo pull", __FILE__, __LINE__));
     }
     for (int k = 0; k < n; ++k) {
         gol_ctx* s = g->shards[k];
@@ -758,32 +797,28 @@ void destroy_impl(gol_ctx* c) {
         g->err = "shard " + std::to_string(c->gindex) + " was destroyed; rebuild the group";
         c->group = nullptr;
     }
-    hipSetDevice(c->device);
-    if (c->compute) hipStreamSynchronize(c->compute);
-    if (c->comm) hipStreamSynchronize(c->comm);
-    if (c->edge) hipStreamSynchronize(c->edge);
-    if (c->xfer) hipStreamSynchronize(c->xfer);
-    if (c->nccl) ncclCommDestroy(c->nccl);
-    for (auto& e : c->evs) {
-        if (e.start) hipEventDestroy(e.start);
-        if (e.stop) hipEventDestroy(e.stop);
+    // gol_destroy returns nothing: a failing teardown call is logged (and
+    // taken off the thread), and teardown goes on.
+    hip_note(hipSetDevice(c->device), "destroy: hipSetDevice");
+    for (hipStream_t st : {c->compute, c->comm, c->edge, c->xfer})
+        if (st) hip_note(hipStreamSynchronize(st), "destroy: hipStreamSynchronize");
+    if (c->nccl) {
+        const ncclResult_t r = ncclCommDestroy(c->nccl);
+        absorb_rccl_status("ncclCommDestroy");
+        if (r != ncclSuccess) fprintf(stderr, "libgol: destroy: ncclCommDestroy: %s\n", ncclGetErrorString(r));
+        c->nccl = nullptr;
     }
-    if (c->ev_ready) hipEventDestroy(c->ev_ready);
-    if (c->ev_halo) hipEventDestroy(c->ev_halo);
-    if (c->ev_edge) hipEventDestroy(c->ev_edge);
-    if (c->ev_snap_ready) hipEventDestroy(c->ev_snap_ready);
-    if (c->ev_snap_done) hipEventDestroy(c->ev_snap_done);
-    if (c->snap) hipFree(c->snap);
-    if (c->clk_buf) hipFree(c->clk_buf);
-    for (auto* p : c->plane) if (p) hipFree(p);
-    if (c->halo_top) hipFree(c->halo_top);
-    if (c->halo_bot) hipFree(c->halo_bot);
-    if (c->zero_row) hipFree(c->zero_row);
-    if (c->slots) hipFree(c->slots);
-    if (c->compute) hipStreamDestroy(c->compute);
-    if (c->comm) hipStreamDestroy(c->comm);
-    if (c->edge) hipStreamDestroy(c->edge);
-    if (c->xfer) hipStreamDestroy(c->xfer);
+    for (auto& e : c->evs) {
+        if (e.start) hip_note(hipEventDestroy(e.start), "destroy: hipEventDestroy");
+        if (e.stop) hip_note(hipEventDestroy(e.stop), "destroy: hipEventDestroy");
+    }
+    for (hipEvent_t ev : {c->ev_ready, c->ev_halo, c->ev_edge, c->ev_snap_ready, c->ev_snap_done})
+        if (ev) hip_note(hipEventDestroy(ev), "destroy: hipEventDestroy");
+    for (void* p : {(void*)c->snap, (void*)c->clk_buf, (void*)c->plane[0], (void*)c->plane[1], (void*)c->halo_top,
+                    (void*)c->halo_bot, (void*)c->zero_row, (void*)c->slots})
+        if (p) hip_note(hipFree(p), "destroy: hipFree");
+    for (hipStream_t st : {c->compute, c->comm, c->edge, c->xfer})
+        if (st) hip_note(hipStreamDestroy(st), "destroy: hipStreamDestroy");
     delete c;
 }
 
@@ -827,7 +862,10 @@ const char* gol_last_error(const gol_ctx* ctx) {
 int gol_device_count(int* count) {
     if (!count) return set_err(nullptr, GOL_EINVAL, "count is null");
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();  // no device: the answer is 0, not an error
+        n = 0;
+    }
     *count = n;
     return GOL_OK;
 }
@@ -862,8 +900,10 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     if (wwords > (1 << 30) || rows > (1 << 30))
         return set_err(nullptr, GOL_EINVAL, "board too large");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
         return set_err(nullptr, GOL_ENODEV, "no HIP device available (libgol has no CPU fallback)");
+    }
     if (c.device < 0 || c.device >= ndev)
         return set_err(nullptr, GOL_EINVAL, "device %d out of range (%d devices)", c.device, ndev);
 
@@ -882,10 +922,13 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     ctx->pairs = c.topology == GOL_TORUS && wwords % 2 == 0;
     ctx->device = c.device;
     ctx->vec_fixed = 0;
-    if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess)
+    if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess) {
+        (void)hipGetLastError();  // unknown CU count: the tuning falls back to its defaults
         ctx->num_cus = 0;
+    }
 
     auto fail = [&](int rc) {
+        (void)hipGetLastError();  // the failed call's status: reported through rc
         std::string msg = ctx->err;
         destroy_impl(ctx);
         set_err(nullptr, rc, "%s", msg.c_str());
@@ -1040,12 +1083,14 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     const size_t bytes = (size_t)ext * ctx->pitch * sizeof(uint32_t);
     uint32_t* blk[2] = {nullptr, nullptr};
     auto release = [&]() {
-        hipStreamSynchronize(ctx->compute);
+        hip_note(hipStreamSynchronize(ctx->compute), "replay: hipStreamSynchronize");
         for (auto* b : blk)
-            if (b) hipFree(b);
+            if (b) hip_note(hipFree(b), "replay: hipFree");
     };
     for (auto*& b : blk) {
         if (hipMalloc(&b, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            b = nullptr;
             release();
             return set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes for the light cone failed", bytes);
         }
@@ -1056,6 +1101,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     const int64_t pitch = ctx->pitch, hp = host_pitch_words;
     uint32_t* up = ctx->pairs ? blk[1] : blk[0];
     auto fail_hip = [&](hipError_t e, const char* what) {
+        (void)hipGetLastError();
         release();
         return set_err(ctx, GOL_EHIP, "%s failed: %s", what, hipGetErrorString(e));
     };
@@ -1183,6 +1229,7 @@ int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_wo
     const size_t bytes = (size_t)ctx->rows * ctx->wwords * sizeof(uint32_t);
     if (!ctx->snap) {
         if (hipMalloc(&ctx->snap, bytes) != hipSuccess) {
+            (void)hipGetLastError();
             ctx->snap = nullptr;
             return set_err(ctx, GOL_ENOMEM, "hipMalloc of %zu bytes for the snapshot buffer failed", bytes);
         }
@@ -1221,9 +1268,26 @@ int gol_snapshot_wait(gol_ctx* ctx, uint64_t* epoch_out) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (!ctx->snap_pending) return set_err(ctx, GOL_ESTATE, "no snapshot in flight");
     if (int rc = bind(ctx)) return rc;
-    ctx->snap_pending = false;
+    // The snapshot stays in flight (and the caller keeps its buffer) until the
+    // transfer is known to be over: a failed wait leaves snap_pending set.
     HIP_CHECK(ctx, hipEventSynchronize(ctx->ev_snap_done));
+    ctx->snap_pending = false;
     if (epoch_out) *epoch_out = ctx->snap_epoch;
+    return GOL_OK;
+}
+
+int gol_snapshot_query(gol_ctx* ctx, int* landed) {
+    if (!ctx || !landed) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (!ctx->snap_pending) return set_err(ctx, GOL_ESTATE, "no snapshot in flight");
+    if (int rc = bind(ctx)) return rc;
+    const hipError_t e = hipEventQuery(ctx->ev_snap_done);
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();  // "not yet" is an answer, not an error
+        *landed = 0;
+        return GOL_OK;
+    }
+    HIP_CHECK(ctx, e);
+    *landed = 1;
     return GOL_OK;
 }
 
@@ -1231,6 +1295,7 @@ int gol_host_alloc(size_t bytes, void** out) {
     if (!out || bytes == 0) return set_err(nullptr, GOL_EINVAL, "gol_host_alloc: null pointer or zero size");
     *out = nullptr;
     if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
         *out = nullptr;
         return set_err(nullptr, GOL_ENOMEM, "hipHostMalloc of %zu bytes failed", bytes);
     }
@@ -1238,7 +1303,7 @@ int gol_host_alloc(size_t bytes, void** out) {
 }
 
 void gol_host_free(void* p) {
-    if (p) hipHostFree(p);
+    if (p) hip_note(hipHostFree(p), "gol_host_free: hipHostFree");
 }
 
 int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state) {
@@ -1289,8 +1354,13 @@ int gol_checkpoint_async(gol_ctx* ctx, void* host_out, size_t bytes) {
     h.width = ctx->width; h.height = ctx->height; h.row0 = ctx->row0; h.rows = ctx->rows;
     h.wwords = ctx->wwords; h.epoch = ctx->epoch; h.topology = ctx->topology;
     h.birth = ctx->birth; h.survive = ctx->survive;
-    memcpy(host_out, &h, sizeof h);
-    return gol_snapshot_async(ctx, reinterpret_cast<uint32_t*>(static_cast<char*>(host_out) + sizeof h), ctx->wwords);
+    // The header goes in only once the rows' copy is under way: a failed call
+    // leaves no buffer that looks like a valid checkpoint.
+    memset(host_out, 0, sizeof h);
+    const int rc =
+        gol_snapshot_async(ctx, reinterpret_cast<uint32_t*>(static_cast<char*>(host_out) + sizeof h), ctx->wwords);
+    if (rc == GOL_OK) memcpy(host_out, &h, sizeof h);
+    return rc;
 }
 
 int gol_restore(gol_ctx* ctx, const void* host_in, size_t bytes) {
@@ -1353,6 +1423,7 @@ int gol_profile_enable(gol_ctx* ctx, int enable) {
         if (int rc = bind(ctx)) return rc;
         const size_t bytes = (size_t)kClockSlots * gol::kClockSlotWords * sizeof(unsigned long long);
         if (hipMalloc(&ctx->clk_buf, bytes) != hipSuccess) {
+            (void)hipGetLastError();
             ctx->clk_buf = nullptr;
             return set_err(ctx, GOL_ENOMEM, "clock-probe buffer allocation failed");
         }
@@ -1437,8 +1508,10 @@ int gol_selftest(int device, uint32_t* report) {
     // v_alignbit and SMEM loads the step kernel relies on.
     if (!report) return set_err(nullptr, GOL_EINVAL, "null argument");
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
         return set_err(nullptr, GOL_ENODEV, "no HIP device available");
+    }
     HIP_CHECK(nullptr, hipSetDevice(device));
     uint32_t h_in[64];
     for (int i = 0; i < 64; ++i) h_in[i] = 0x01000193u * (uint32_t)(i + 1) ^ (uint32_t)(i << 24);
@@ -1448,8 +1521,8 @@ int gol_selftest(int device, uint32_t* report) {
     HIP_CHECK(nullptr, hipMemcpy(d_in, h_in, sizeof h_in, hipMemcpyHostToDevice));
     HIP_CHECK(nullptr, gol::launch_selftest(d_in, d_out, nullptr));
     HIP_CHECK(nullptr, hipMemcpy(report, d_out, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    hipFree(d_in);
-    hipFree(d_out);
+    hip_note(hipFree(d_in), "selftest: hipFree");
+    hip_note(hipFree(d_out), "selftest: hipFree");
     return GOL_OK;
 }
 
@@ -1489,23 +1562,49 @@ int gol_group_create(gol_group** out, gol_ctx* const* shards, int n) {
         gol_ctx* dn = g->shards[(k + 1) % n];
         if (s->device != dn->device) {
             int ok = 0;
-            if (hipDeviceCanAccessPeer(&ok, s->device, dn->device) == hipSuccess && ok) {
-                hipSetDevice(s->device);
-                (void)hipDeviceEnablePeerAccess(dn->device, 0);
-                hipSetDevice(dn->device);
-                (void)hipDeviceEnablePeerAccess(s->device, 0);
+            if (hipDeviceCanAccessPeer(&ok, s->device, dn->device) != hipSuccess) {
+                (void)hipGetLastError();
+                ok = 0;
+            }
+            if (ok) {
+                for (auto [from, to] : {std::pair<int, int>{s->device, dn->device}, {dn->device, s->device}}) {
+                    hip_note(hipSetDevice(from), "group: hipSetDevice");
+                    const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+                    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();  // an earlier group did it
+                    else hip_note(e, "group: hipDeviceEnablePeerAccess");
+                }
             }
         }
     }
-    (void)hipGetLastError();  // clear "peer access already enabled"
     *out = g;
     return GOL_OK;
 }
 
 const char* gol_group_last_error(const gol_group* g) { return g ? g->err.c_str() : ""; }
 
+int gol_diag_take_hip_error(int* code) {
+    if (!code) return set_err(nullptr, GOL_EINVAL, "null argument");
+    *code = (int)hipGetLastError();
+    return GOL_OK;
+}
+
+int gol_diag_absorbed(uint64_t* count, char* last, size_t cap) {
+    std::lock_guard<std::mutex> lk(g_absorb_mu);
+    if (count) *count = g_absorbed;
+    if (last && cap > 0) snprintf(last, cap, "%s", g_absorbed_last.c_str());
+    return GOL_OK;
+}
+
 int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
+    return gol_group_step_partials(g, generations, hashes_out, nullptr);
+}
+
+int gol_group_step_partials(gol_group* g, uint32_t generations, uint64_t* hashes_out, uint64_t* partials_out) {
     if (!g) return set_err(nullptr, GOL_EINVAL, "null group");
+    if (partials_out && !hashes_out) {
+        g->err = "partials_out needs hashes_out";
+        return GOL_EINVAL;
+    }
     for (const gol_ctx* s : g->shards)
         if (!s) return GOL_ESTATE;  // g->err names the lost shard
     if (generations == 0) return GOL_OK;
@@ -1520,8 +1619,8 @@ int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
             for (gol_ctx* s : g->shards) {
                 if (int rc = bind(s)) return group_fail(g, s, rc);
                 if (int rc = ensure_slots(s, cnt)) return group_fail(g, s, rc);
-                if (hipMemsetAsync(s->slots, 0, cnt * per * sizeof(unsigned long long), s->compute) != hipSuccess)
-                    return group_fail(g, s, set_err(s, GOL_EHIP, "hipMemsetAsync failed"));
+                if (hipError_t e = hipMemsetAsync(s->slots, 0, cnt * per * sizeof(unsigned long long), s->compute))
+                    return group_fail(g, s, hip_fail(s, e, "hipMemsetAsync", __FILE__, __LINE__));
                 base.push_back(s->slots);
             }
         }
@@ -1538,12 +1637,14 @@ int gol_group_step(gol_group* g, uint32_t generations, uint64_t* hashes_out) {
             for (int k = 0; k < n; ++k) {
                 gol_ctx* s = g->shards[k];
                 if (int rc = bind(s)) return group_fail(g, s, rc);
-                if (hipMemcpyAsync(s->host_slots.data(), s->slots, cnt * per * sizeof(unsigned long long),
-                                   hipMemcpyDeviceToHost, s->compute) != hipSuccess ||
-                    hipStreamSynchronize(s->compute) != hipSuccess)
-                    return group_fail(g, s, set_err(s, GOL_EHIP, "hash readback failed"));
+                hipError_t e = hipMemcpyAsync(s->host_slots.data(), s->slots, cnt * per * sizeof(unsigned long long),
+                                              hipMemcpyDeviceToHost, s->compute);
+                if (e == hipSuccess) e = hipStreamSynchronize(s->compute);
+                if (e != hipSuccess) return group_fail(g, s, hip_fail(s, e, "hash readback", __FILE__, __LINE__));
                 fold_slots(s, cnt, part.data());
                 for (uint32_t j = 0; j < cnt; ++j) hashes_out[g0 + j] += part[j];
+                if (partials_out)
+                    std::copy(part.begin(), part.end(), partials_out + (size_t)k * generations + g0);
             }
         }
     }
@@ -1563,9 +1664,9 @@ void gol_group_destroy(gol_group* g) {
     if (!g) return;
     for (gol_ctx* s : g->shards) {
         if (!s) continue;
-        hipSetDevice(s->device);
-        hipStreamSynchronize(s->comm);
-        hipStreamSynchronize(s->compute);
+        hip_note(hipSetDevice(s->device), "group destroy: hipSetDevice");
+        hip_note(hipStreamSynchronize(s->comm), "group destroy: hipStreamSynchronize");
+        hip_note(hipStreamSynchronize(s->compute), "group destroy: hipStreamSynchronize");
         s->group = nullptr;
         s->gindex = 0;
     }

@@ -4,6 +4,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+#include <type_traits>
+#include <utility>
+
 namespace gol {
 
 constexpr int kWaveLanes = 64;   // CDNA wavefront
@@ -27,14 +31,23 @@ constexpr uint32_t kHashRowMul = 0x9E3779B1u;
 constexpr uint32_t kHashOddAdd = 0x6A09E666u;
 constexpr uint32_t kHashPairAdd = 0x7F4A7C15u;
 
-// hipGetLastError() after a launch also returns an error left behind by any
-// earlier runtime call of this thread whose status its caller discarded (an
-// occupancy query, a teardown call, another library's probe), which would
-// then be pinned on the launch.  Every launch helper therefore drops such a
-// stale status first (reported once per error code on stderr) so its check
-// reports the launch alone; a device fault still surfaces at the next
-// synchronising call, which every entry point checks.
-void drop_stale_error();
+// Launch `kernel` and return the status of this launch alone.
+// hipLaunchKernel returns it directly; hipGetLastError() after a
+// triple-chevron launch would instead report -- and clear -- whatever status
+// an earlier call of this thread left pending (DESIGN.md section 2 "HIP
+// status discipline").  The arguments are converted to the kernel's parameter
+// types first, as a direct call would.
+template <typename... KArgs, typename... Args>
+hipError_t launch_kernel(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t stream, Args&&... args) {
+    static_assert(sizeof...(KArgs) == sizeof...(Args), "kernel argument count");
+    std::tuple<std::remove_cv_t<KArgs>...> vals(std::forward<Args>(args)...);
+    return std::apply(
+        [&](auto&... v) {
+            void* argv[] = {static_cast<void*>(&v)...};
+            return hipLaunchKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, 0, stream);
+        },
+        vals);
+}
 
 __host__ __device__ __forceinline__ uint32_t hash_row_key(int64_t y) {
     const uint32_t t = (uint32_t)y * kHashRowMul;

@@ -1,8 +1,6 @@
 // gol_misc.hip -- board seeding, standalone state hash, the cross-lane self
 // test, and the launch dispatcher over pass depths.
 #include <algorithm>
-#include <atomic>
-#include <cstdio>
 
 #include "gol_stencil.h"
 
@@ -136,15 +134,6 @@ hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool h
     }
 }
 
-void drop_stale_error() {
-    const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) return;
-    static std::atomic<uint64_t> seen{0};
-    const uint64_t bit = 1ull << ((unsigned)e % 64u);
-    if (!(seen.fetch_or(bit) & bit))
-        fprintf(stderr, "libgol: dropped a stale HIP status before a launch: %s (%d)\n", hipGetErrorString(e), (int)e);
-}
-
 int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, bool pairs) {
     switch (gens) {
         case 1: return blocks_step_g1(vec, variant, life, hash, clipped, pairs);
@@ -167,10 +156,8 @@ hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t w
                        uint64_t seed, bool pairs, hipStream_t stream) {
     const int64_t total = (int64_t)rows * wwords;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
-    drop_stale_error();
-    hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(256), 0, stream, plane, pitch, wwords, width, grow0, rows,
-                       seed, pairs ? 1 : 0);
-    return hipGetLastError();
+    return launch_kernel(seed_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, width, grow0, rows, seed,
+                         pairs ? 1 : 0);
 }
 
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
@@ -179,25 +166,19 @@ hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int
     if (wwords % 2 != 0) return hipErrorInvalidValue;
     const int64_t total = (int64_t)rows * (wwords / 2);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
-    drop_stale_error();
-    hipLaunchKernelGGL(convert_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, pitch, dst_pitch, wwords / 2,
-                       rows, to_pairs ? 1 : 0);
-    return hipGetLastError();
+    return launch_kernel(convert_kernel, dim3(blocks), dim3(256), stream, src, dst, pitch, dst_pitch, wwords / 2, rows,
+                         to_pairs ? 1 : 0);
 }
 
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0, int32_t rows,
                        unsigned long long* slots, hipStream_t stream) {
     const int64_t total = (int64_t)rows * wwords;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
-    drop_stale_error();
-    hipLaunchKernelGGL(hash_kernel, dim3(blocks), dim3(256), 0, stream, plane, pitch, wwords, grow0, rows, slots);
-    return hipGetLastError();
+    return launch_kernel(hash_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, grow0, rows, slots);
 }
 
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream) {
-    drop_stale_error();
-    hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 0, stream, in, out);
-    return hipGetLastError();
+    return launch_kernel(selftest_kernel, dim3(1), dim3(64), stream, in, out);
 }
 
 }  // namespace gol

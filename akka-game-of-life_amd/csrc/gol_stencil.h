@@ -1017,42 +1017,37 @@ constexpr bool kHgLanes = VEC <= 2;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
-    drop_stale_error();
+    const dim3 grid(gx, gy), block(kWaveLanes * kWavesPerWG);
     if constexpr (G == 1) {
-        hipLaunchKernelGGL((step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
-                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
-    } else if (kHgLanes<VEC> && p.variant == 2) {
-        if constexpr (kHgLanes<VEC>) {
-            hipLaunchKernelGGL((multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
-                               dim3(kWaveLanes * kWavesPerWG), 0, st, p);
-        }
+        return launch_kernel(step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
     } else {
-        hipLaunchKernelGGL((multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>), dim3(gx, gy),
-                           dim3(kWaveLanes * kWavesPerWG), 0, st, p);
+        if constexpr (kHgLanes<VEC>) {
+            if (p.variant == 2)
+                return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
+        }
+        return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
     }
-    return hipGetLastError();
 }
 
 // Resident 256-thread workgroups per CU for a kernel instance (occupancy API).
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
 int blocks_one(int variant) {
-    int n = 0;
-    hipError_t e;
+    auto query = [](auto kernel) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kWaveLanes * kWavesPerWG, 0) != hipSuccess) {
+            (void)hipGetLastError();  // the failed query's own status: reported as 0 (unknown), not left pending
+            return 0;
+        }
+        return n;
+    };
     if constexpr (G == 1) {
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>,
-                                                         kWaveLanes * kWavesPerWG, 0);
+        return query(step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>);
     } else {
         if constexpr (kHgLanes<VEC>) {
-            if (variant == 2) {
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &n, multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, kWaveLanes * kWavesPerWG, 0);
-                return e == hipSuccess ? n : 0;
-            }
+            if (variant == 2) return query(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>);
         }
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>,
-                                                         kWaveLanes * kWavesPerWG, 0);
+        return query(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>);
     }
-    return e == hipSuccess ? n : 0;
 }
 
 // The instances a launch can select: clipped boards (generic rule, row-major

@@ -81,6 +81,7 @@ _SIGNATURES = {
     "gol_snapshot_async": (_c.c_int, [_vp, _u32p, _c.c_int64]),
     "gol_checkpoint_async": (_c.c_int, [_vp, _vp, _c.c_size_t]),
     "gol_snapshot_wait": (_c.c_int, [_vp, _u64p]),
+    "gol_snapshot_query": (_c.c_int, [_vp, ctypes.POINTER(_c.c_int)]),
     "gol_host_alloc": (_c.c_int, [_c.c_size_t, ctypes.POINTER(_vp)]),
     "gol_host_free": (None, [_vp]),
     "gol_get_cell": (_c.c_int, [_vp, _c.c_int64, _c.c_int64, ctypes.POINTER(_c.c_int)]),
@@ -102,9 +103,12 @@ _SIGNATURES = {
                                  ctypes.POINTER(_c.c_int32)]),
     "gol_group_create": (_c.c_int, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _c.c_int]),
     "gol_group_step": (_c.c_int, [_vp, _c.c_uint32, _u64p]),
+    "gol_group_step_partials": (_c.c_int, [_vp, _c.c_uint32, _u64p, _u64p]),
     "gol_group_sync": (_c.c_int, [_vp]),
     "gol_group_last_error": (_c.c_char_p, [_vp]),
     "gol_group_destroy": (None, [_vp]),
+    "gol_diag_take_hip_error": (_c.c_int, [ctypes.POINTER(_c.c_int)]),
+    "gol_diag_absorbed": (_c.c_int, [_u64p, _c.c_char_p, _c.c_size_t]),
 }
 
 
@@ -163,3 +167,20 @@ def unique_id() -> bytes:
     buf = (ctypes.c_uint8 * GOL_UNIQUE_ID_BYTES)()
     check(lib.gol_comm_unique_id(buf))
     return bytes(buf)
+
+
+def take_hip_error() -> int:
+    """The calling thread's pending HIP status (0: none), taken off the
+    thread (gol_diag_take_hip_error)."""
+    c = ctypes.c_int(0)
+    check(lib.gol_diag_take_hip_error(ctypes.byref(c)))
+    return c.value
+
+
+def absorbed() -> tuple[int, str]:
+    """(count, last description) of the HIP statuses RCCL calls left behind
+    and libgol absorbed (gol_diag_absorbed)."""
+    n = ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(256)
+    check(lib.gol_diag_absorbed(ctypes.byref(n), buf, len(buf)))
+    return n.value, buf.value.decode()

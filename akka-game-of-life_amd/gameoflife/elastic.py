@@ -140,6 +140,34 @@ def covering_epochs(ckpt_dir: str, lo: int, hi: int) -> list[int]:
     return out
 
 
+def light_cone_ranges(lo: int, hi: int, depth: int, height: int, torus: bool) -> list[tuple[int, int]]:
+    """Row intervals of [0, height) that block [lo, hi) and its `depth`-row
+    light cone on each side occupy (mod the height on a torus, clipped at a
+    clipped board's edges)."""
+    a, b = lo - depth, hi + depth
+    if not torus:
+        return [(max(a, 0), min(b, height))]
+    n = b - a
+    if n >= height:
+        return [(0, height)]
+    a %= height
+    return [(a, a + n)] if a + n <= height else [(a, height), (0, a + n - height)]
+
+
+def recovery_epoch(ckpt_dir: str, lo: int, hi: int, epoch: int, height: int, torus: bool) -> int:
+    """The latest checkpoint epoch c <= `epoch` from which block [lo, hi) can
+    be replayed to `epoch`: the files of c must hold the block AND its light
+    cone, the epoch - c rows on each side.  The block's own file alone is not
+    enough -- a backend killed at a checkpoint epoch dies before writing its
+    file, so a neighbour lost later may find its own rows at an epoch whose
+    light cone is incomplete."""
+    for c in sorted((e for e in covering_epochs(ckpt_dir, lo, hi) if e <= epoch), reverse=True):
+        files = _shard_files(ckpt_dir, c)
+        if all(_covers(files, a, b) for a, b in light_cone_ranges(lo, hi, epoch - c, height, torus)):
+            return c
+    raise FileNotFoundError(f"no checkpoint epoch <= {epoch} holds rows [{lo}, {hi}) and their light cone")
+
+
 def blob_rows(blobs, indices) -> np.ndarray:
     """Rows `indices` (global row numbers) cut from checkpoint blobs of one
     epoch (any decomposition; blocks may overlap)."""
@@ -343,6 +371,7 @@ def worker_main(a) -> int:
         shard.restore(make_checkpoint(dict(h, epoch=a.target), cur))
         epoch = a.target
         extra["replayed"] = {"from": a.resume, "to": a.target, "partials": [str(int(x)) for x in hs]}
+        write_shard_checkpoint(a.ckpt_dir, shard.checkpoint())  # the next loss replays from here
     shard.join(a.ring_dir, rank, world)
     report(0, epoch)
     seq = 0
@@ -396,6 +425,9 @@ def worker_main(a) -> int:
             shard.restore(make_checkpoint(dict(mine_h, row0=row0, rows=rows, epoch=epoch), merged))
             extra["replayed"] = {"from": c, "to": epoch, "row0": lo, "rows": n_lost,
                                  "partials": [str(int(x)) for x in hs]}
+            # the merged block's rows at this epoch, so a later loss next to
+            # it finds a complete light cone without going back past it
+            write_shard_checkpoint(a.ckpt_dir, shard.checkpoint())
             world = 1
         elif op == "rejoin":
             shard.leave()
@@ -509,8 +541,7 @@ class Supervisor:
         for w in lost:
             self.workers.remove(w)
         for w in sorted(lost, key=lambda w: w.row0):
-            eps = [e for e in covering_epochs(self.ckpt_dir, w.row0, w.row0 + w.rows) if e <= epoch]
-            c = eps[-1]
+            c = recovery_epoch(self.ckpt_dir, w.row0, w.row0 + w.rows, epoch, self.height, self.topology == "torus")
             ev = {"event": "lost", "worker": w.wid, "rows": [w.row0, w.row0 + w.rows], "epoch": epoch,
                   "checkpoint_epoch": c, "replayed_generations": epoch - c}
             above = [s for s in self.workers if s.row0 + s.rows == w.row0]
@@ -634,6 +665,9 @@ def _parser():
     dm.add_argument("--world", type=int, default=8)
     dm.add_argument("--kill", default="3@25", help="crash rank@generation, or 'none'")
     dm.add_argument("--workdir", default="/tmp/gol_elastic")
+    dm.add_argument("--chunk", type=int, default=5, help="generations per supervisor release")
+    dm.add_argument("--shard", default="gameoflife.elastic:GpuShard",
+                    help="backend implementation module:Class (the CPU tests pass their oracle double)")
     return ap
 
 
@@ -642,9 +676,10 @@ def main(argv=None) -> int:
     if a.cmd == "worker":
         return worker_main(a)
     kill = None if a.kill == "none" else tuple(int(x) for x in a.kill.split("@"))
-    sup = Supervisor(a.width, a.height, a.gens, a.world, a.workdir, a.every, kill=kill, chunk=5)
+    sup = Supervisor(a.width, a.height, a.gens, a.world, a.workdir, a.every, kill=kill, chunk=a.chunk, shard=a.shard)
     got = sup.run()
-    ref = Supervisor(a.width, a.height, a.gens, a.world, a.workdir + "_ref", a.every, chunk=5).run()
+    ref = Supervisor(a.width, a.height, a.gens, a.world, a.workdir + "_ref", a.every, chunk=a.chunk,
+                     shard=a.shard).run()
     same = [got.get(e) == ref.get(e) for e in range(1, a.gens + 1)]
     print(json.dumps({"events": sup.events, "generations": a.gens, "hashes_equal": all(same)}))
     return 0 if all(same) else 1

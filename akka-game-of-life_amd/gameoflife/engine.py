@@ -101,6 +101,13 @@ class GolEngine:
             self._snap_out = None
         return e.value
 
+    def snapshot_landed(self) -> bool:
+        """Has the snapshot started by snapshot_async reached its buffer?
+        (gol_snapshot_query: non-blocking; snapshot_wait still ends it)."""
+        d = ctypes.c_int(0)
+        self._chk(N.lib.gol_snapshot_query(self._h, ctypes.byref(d)))
+        return bool(d.value)
+
     def host_buffer(self) -> np.ndarray:
         """A page-locked (rows, wwords) uint32 buffer for snapshots / loads."""
         return host_array((self.rows, self.wwords))
@@ -243,8 +250,16 @@ class ShardGroup:
         if rc != N.GOL_OK:
             raise N.GolError(rc, (N.lib.gol_group_last_error(self._h) or b"").decode())
 
-    def step(self, generations: int = 1, hashes: bool = False):
-        """Advance every shard; returns the global per-generation hashes if asked."""
+    def step(self, generations: int = 1, hashes: bool = False, partials: bool = False):
+        """Advance every shard; returns the global per-generation hashes if
+        asked, and with partials=True also every shard's partials as a
+        (shards, generations) array (gol_group_step_partials)."""
+        if partials:
+            out = np.zeros(generations, dtype=np.uint64)
+            part = np.zeros((len(self.shards), generations), dtype=np.uint64)
+            self._chk(N.lib.gol_group_step_partials(self._h, generations, out.ctypes.data_as(N._u64p),
+                                                    part.ctypes.data_as(N._u64p)))
+            return out, part
         if hashes:
             out = np.zeros(generations, dtype=np.uint64)
             self._chk(N.lib.gol_group_step(self._h, generations, out.ctypes.data_as(N._u64p)))

@@ -61,11 +61,13 @@ class ShardedSimulation:
             s.seed(seed)
         self.group: ShardGroup | None = ShardGroup(self.shards)
         self.hashes: list[int] = []          # global per-generation hashes, epochs 1..epoch
+        self.partials: dict[int, list[int]] = {}  # epoch -> every shard's partial hash (since the last checkpoint)
         self.epoch = 0
         self.ckpt_epoch = -1
         self.ckpt: list[bytes] = []
         self.events: list[str] = []
         self.checkpoint()
+        self._finish_checkpoint()  # epoch 0 is a recovery point before anything can be lost
 
     def _make(self, k: int, device: int) -> GolEngine:
         row0, rows = shard_rows_py(self.height, k, self.n)
@@ -98,9 +100,30 @@ class ShardedSimulation:
         epoch, self._pending_epoch = self._pending_epoch, None
         self._commit_checkpoint(list(blobs), epoch)
 
+    def _drop_checkpoint(self, lost: int, landed: bool | None = None) -> None:
+        """Shard `lost` dies while a background checkpoint may be in flight.
+        If its part has reached host memory (gol_snapshot_query; `landed`
+        forces the answer) the set is complete and is committed; otherwise
+        that part never lands, so the set is discarded (the survivors' copies
+        are waited for, to release their buffers) and the previous committed
+        checkpoint stays the recovery point."""
+        if self._pending_epoch is None:
+            return
+        if landed is None:
+            landed = self.shards[lost].snapshot_landed()
+        if landed:
+            self._finish_checkpoint()
+            return
+        for j, s in enumerate(self.shards):
+            if j != lost:
+                s.snapshot_wait()
+        self.events.append(f"checkpoint@{self._pending_epoch} dropped (shard {lost} lost in flight)")
+        self._pending_epoch = None  # the set is rewritten by the next checkpoint
+
     def _commit_checkpoint(self, blobs: list, epoch: int) -> None:
         self.ckpt = blobs
         self.ckpt_epoch = epoch
+        self.partials = {e: p for e, p in self.partials.items() if e > epoch}
         if self.checkpoint_dir:
             os.makedirs(self.checkpoint_dir, exist_ok=True)
             for k, blob in enumerate(self.ckpt):
@@ -120,7 +143,10 @@ class ShardedSimulation:
             k = self.checkpoint_every
             to_ckpt = (k - self.epoch % k) if k else generations
             n = min(generations, to_ckpt)
-            hs = [int(h) for h in self.group.step(n, hashes=True)]
+            glob, part = self.group.step(n, partials=True)
+            hs = [int(h) for h in glob]
+            for g in range(n):
+                self.partials[self.epoch + g + 1] = [int(x) for x in part[:, g]]
             self.epoch += n
             self.hashes.extend(hs)
             out.extend(hs)
@@ -130,9 +156,12 @@ class ShardedSimulation:
         return out
 
     # ---------------------------------------------------------------- faults
-    def kill(self, k: int) -> None:
-        """Lose shard k (its context and device memory are gone)."""
-        self._finish_checkpoint()
+    def kill(self, k: int, checkpoint_landed: bool | None = None) -> None:
+        """Lose shard k (its context and device memory are gone).  A
+        background checkpoint still in flight on shard k is lost with it
+        (checkpoint_landed: force whether it had landed; None asks the
+        device)."""
+        self._drop_checkpoint(k, checkpoint_landed)
         self.shards[k].close()            # the group now has a hole (gol_group_step -> GOL_ESTATE)
         self.shards[k] = None
         self.group.close()
@@ -182,6 +211,14 @@ class ShardedSimulation:
         up, dn = light_cone_from(lambda idx: blob_rows(blobs, idx), s.row0, s.rows, d, self.height,
                                  self.topology == "torus", s.wwords)
         part = [int(h) for h in s.replay(d, up, dn)] if d else []
+        # the replayed partials must complete the global hashes recorded
+        # before the loss: survivors' partials + shard k's == global, mod 2^64
+        for g, p in enumerate(part, start=self.ckpt_epoch + 1):
+            others = sum(v for j, v in enumerate(self.partials[g]) if j != k)
+            if (others + p) % (1 << 64) != self.hashes[g - 1]:
+                raise AssertionError(f"replayed partial of shard {k} at generation {g} does not complete "
+                                     "the recorded global hash")
+            self.partials[g][k] = p
         self.group = ShardGroup(self.shards)
         self.events.append(f"respawn shard {k} on device {device}, light cone {self.ckpt_epoch}->{self.epoch}")
         return part

@@ -20,10 +20,10 @@ N = 1, a shard's interior-rows launch at N > 1) is bound by VALU issue, not by
 HBM -- temporal blocking fuses 6-8 generations per pass over the plane.  So:
   * roofline.bound = "valu": achieved = cell-updates per second of that launch
     (cells x generations per launch / its mean HIP-event duration), peak = the
-    VALU-issue ceiling of the kernel's loop mix at the clock the chip held
-    during those launches (an in-kernel probe of the timed launches,
-    gol_profile_clock; PMC GRBM_GUI_ACTIVE from profiles/pmc_launch.json
-    beside it as clock_pmc_ghz);
+    VALU-issue ceiling of the kernel's loop mix at the guide's 2.4 GHz max
+    clock, frac = achieved / peak; roofline.held_clock prices the same launches
+    at the clock they actually held (in-kernel probe, gol_profile_clock) as an
+    issue-efficiency diagnostic, with the PMC clock (profiles/) beside it;
   * roofline.traffic = PMC HBM bytes per launch, and roofline.hbm the physical
     HBM bandwidth that implies against the 8 TB/s spec;
   * roofline.hbm_effective = SURVEY.md section 8(d)'s 2 bits per cell-update,
@@ -95,15 +95,17 @@ def barrier(dist, world):
 
 
 def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
-    if warmup > 0:
-        eng.step(warmup, hashes=with_hash)
+    """W untimed + K timed generations.  Returns (seconds, kernel ms,
+    launches, generations covered by them, probe clock GHz, hashes): hashes
+    = the W + K per-generation partial hashes of this shard when with_hash."""
+    hw = eng.step(warmup, hashes=with_hash) if warmup > 0 else None
     eng.sync()
     eng.profile(True)
     eng.profile_reset()
     barrier(dist, world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    eng.step(steps, hashes=with_hash)
+    ht = eng.step(steps, hashes=with_hash)
     eng.sync()
     torch.cuda.synchronize()
     # the clock stops when this rank's work is done; the closing barrier and
@@ -121,7 +123,76 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         timed_run.rank_times = [float(x) for x in t.tolist()]
         dt = max(timed_run.rank_times)
-    return dt, kms, launches, gens, clock
+    hashes = None
+    if with_hash:
+        import numpy as np
+        hashes = np.concatenate([h for h in (hw, ht) if h is not None]).astype(np.uint64)
+    return dt, kms, launches, gens, clock, hashes
+
+
+GOLDEN_SEED = 0x5EED
+
+
+def golden_hashes(W, H):
+    """Global state hashes of the bench board (W x H torus, B3/S23, seed
+    0x5EED) at epochs 0, 1, ..., from tests/golden/bench_<W>.json -- written by
+    tests/golden/make_bench_golden.py with the CPU oracle (a data file: bench
+    never runs the oracle to check itself).  None if there is no table."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", f"bench_{W}.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("board") != [W, H] or d.get("seed") != GOLDEN_SEED or d.get("rule") != "B3/S23":
+        return None
+    return [int(x, 16) for x in d["hashes"]]
+
+
+def global_hash(eng, world):
+    """The whole board's state hash: gol_hash of every shard, summed over the
+    ranks with gol_comm_allreduce_u64 (RCCL) -- the hash is a sum mod 2^64, so
+    the N shards' partials add up to the N = 1 value."""
+    import numpy as np
+    h = np.array([eng.hash()], dtype=np.uint64)
+    if world > 1:
+        h = eng.allreduce_u64(h)
+    return int(h[0])
+
+
+class Parity:
+    """bench.py's self-check against the committed golden hashes: every rank's
+    shard is checked at every N, so the multi-GPU line records whether the RCCL
+    halo exchange kept the board bit-exact (CellActor.scala:71-77,
+    NextStateCellGathererActor.scala:32-36 are the exchange it replaces)."""
+
+    def __init__(self, W, H):
+        self.golden = golden_hashes(W, H)
+        self.checks = []
+
+    def _golden(self, epoch):
+        return self.golden[epoch] if self.golden is not None and epoch < len(self.golden) else None
+
+    def board(self, what, epoch, value):
+        g = self._golden(epoch)
+        self.checks.append({"what": what, "epoch": epoch, "hash": f"{value:#018x}",
+                            "golden": None if g is None else f"{g:#018x}",
+                            "match": None if g is None else value == g})
+
+    def sequence(self, what, first_epoch, values):
+        gs = [self._golden(first_epoch + k) for k in range(len(values))]
+        known = [(first_epoch + k, int(v), g) for k, (v, g) in enumerate(zip(values, gs)) if g is not None]
+        bad = [e for e, v, g in known if v != g]
+        self.checks.append({"what": what, "epochs": [first_epoch, first_epoch + len(values) - 1],
+                            "checked": len(known), "mismatched_epochs": bad[:16],
+                            "last_hash": f"{int(values[-1]):#018x}" if len(values) else None,
+                            "match": (not bad) if known else None})
+
+    def report(self):
+        ms = [c["match"] for c in self.checks]
+        return {"golden": "tests/golden/bench_262144.json (CPU oracle, tests/golden/make_bench_golden.py; "
+                          "parity unpinned: the reference ships no vectors)" if self.golden else None,
+                "checks": self.checks,
+                "match": None if not ms or any(m is None for m in ms) else all(ms)}
 
 
 def cpu_model():
@@ -135,29 +206,40 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(width, seconds):
-    """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
-    workload: a torus of the same width and 1024 rows, run for ~`seconds`, on
-    every core this process may use -- the CPU share the harness grants the
-    job (OMP_NUM_THREADS, 16 threads per GPU on the pool's boxes), else every
-    core of sched_getaffinity."""
-    from oracle import oracle as O
-    affinity = len(os.sched_getaffinity(0))
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(share, affinity) if share > 0 else affinity
-    H = 1024
-    board = O.seed_packed(width, H, 0x5EED)
+def _cpu_rate(O, width, H, threads, seconds):
+    board = O.seed_packed(width, H, GOLDEN_SEED)
     O.run_packed(board, width, 1, nthreads=threads, want_hashes=False)  # warm
     gens, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         board, _ = O.run_packed(board, width, 4, nthreads=threads, want_hashes=False)
         gens += 4
     dt = time.perf_counter() - t0
-    return {"value": round(width * H * gens / dt / 1e9, 3), "unit": "GCUPS", "cores": threads,
-            "kind": "port", "nproc": affinity, "cpu_model": cpu_model(),
-            "threads_source": "OMP_NUM_THREADS (the job's CPU share)" if share > 0 else "sched_getaffinity",
-            "sample": f"oracle_run_packed (oracle/gol_oracle.c, bit-sliced, OpenMP), {width}x{H} torus B3/S23 "
-                      f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
+    return width * H * gens / dt / 1e9, gens, dt
+
+
+def cpu_baseline(width, seconds):
+    """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
+    workload: a torus of the same width and 1024 rows, run for ~`seconds`.
+    The reported value uses the CPU share the harness grants the job
+    (OMP_NUM_THREADS: 16 threads per GPU on the pool's boxes); a shorter
+    sample on every core of sched_getaffinity (all
+    host cores) is reported beside it when that is more threads."""
+    from oracle import oracle as O
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(share, affinity) if share > 0 else affinity
+    H = 1024
+    v, gens, dt = _cpu_rate(O, width, H, threads, seconds)
+    out = {"value": round(v, 3), "unit": "GCUPS", "cores": threads,
+           "kind": "port", "nproc": os.cpu_count(), "affinity": affinity, "cpu_model": cpu_model(),
+           "threads_source": "OMP_NUM_THREADS (the job's CPU share)" if share > 0 else "sched_getaffinity",
+           "sample": f"oracle_run_packed (oracle/gol_oracle.c, bit-sliced, OpenMP), {width}x{H} torus B3/S23 "
+                     f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
+    if affinity > threads:
+        va, ga, dta = _cpu_rate(O, width, H, affinity, max(seconds / 3, 1.0))
+        out["all_affinity"] = {"value": round(va, 3), "unit": "GCUPS", "cores": affinity,
+                               "sample": f"same slice, {ga} generations in {dta:.1f} s on {affinity} threads"}
+    return out
 
 
 def pmc_launch():
@@ -204,8 +286,8 @@ def compact_plan(plan):
 
 def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None):
     """Roofline of the dominant kernel (see the module docstring).  `clock`:
-    GHz the timed launches ran at, from the in-kernel probe
-    (gol_profile_clock); the PMC table's clock is the fallback."""
+    GHz the timed launches held, from the in-kernel probe (gol_profile_clock):
+    it prices the held_clock diagnostic, never the primary frac."""
     if not launches:
         return None
     avg_s = kms / 1e3 / launches
@@ -226,26 +308,27 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
             r["traffic_source"] = "profiles/pmc_launch.json " + ", ".join(pmc["keys"])
         return r
     mix = VALU_MIX_HASH if hashed else VALU_MIX
-    live = bool(clock)
-    if not live:
-        clock = pmc["clock_ghz"] if pmc else CLOCK_MAX_GHZ
-    peak, cycles = valu_peak_gcups(mix, clock)
-    peak_max, _ = valu_peak_gcups(mix, CLOCK_MAX_GHZ)
-    r = {"bound": "valu", "achieved": round(gcups, 1), "peak": round(peak, 1), "unit": "GCUPS",
-         "frac": round(gcups / peak, 4), "traffic": round(pmc["hbm_bytes"]) if pmc else None,
-         "clock_ghz": round(clock, 3),
-         "clock_source": ("in-kernel probe of these timed launches: every workgroup's core-clock (s_memtime) "
-                          "and 100 MHz reference (s_memrealtime) ticks, summed (gol_profile_clock)") if live else
-                         ("PMC GRBM_GUI_ACTIVE / 8 / launch time, time-weighted over the plan "
-                          "(profiles/pmc_launch.json)") if pmc else "max clock (no PMC entry for this plan)",
-         "clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None,
-         "frac_at_max_clock": round(gcups / peak_max, 4),
+    # frac: against the VALU-issue ceiling at the guide's max clock (2.4 GHz,
+    # MI355X_MICROARCH.md) -- the peak the chip is specified for.  The clock
+    # these launches actually held (in-kernel probe, gol_profile_clock) only
+    # prices the separate issue-efficiency diagnostic under held_clock.
+    peak_max, cycles = valu_peak_gcups(mix, CLOCK_MAX_GHZ)
+    r = {"bound": "valu", "achieved": round(gcups, 1), "peak": round(peak_max, 1), "unit": "GCUPS",
+         "frac": round(gcups / peak_max, 4), "traffic": round(pmc["hbm_bytes"]) if pmc else None,
+         "peak_clock_ghz": CLOCK_MAX_GHZ,
          "valu": {"instructions_per_word_generation": {k: n for k, (n, _) in mix.items()},
                   "cycles_per_word_generation": round(cycles, 2),
-                  "peak_gcups_at_max_clock": round(peak_max, 1),
                   "measured_valu_per_word_generation": round(pmc["valu_per_word_gen"], 2) if pmc else None,
                   "source": "loop census scripts/isa_loop.py; issue costs profiles/r01_valu_op_costs.txt"},
          **common}
+    held = {"clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None}
+    if clock:
+        peak_held, _ = valu_peak_gcups(mix, clock)
+        held.update({"ghz": round(clock, 3), "peak_at_held_clock": round(peak_held, 1),
+                     "issue_efficiency": round(gcups / peak_held, 4),
+                     "source": "in-kernel probe of these timed launches: every sampled workgroup's core-clock "
+                               "(s_memtime) and 100 MHz reference (s_memrealtime) ticks, summed (gol_profile_clock)"})
+    r["held_clock"] = held
     if pmc:
         gbs = pmc["hbm_bytes"] / avg_s / 1e9
         r["hbm"] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -301,10 +384,10 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
         e2.seed(0x5EED)
         n_s, w_s = max(a.steps, 102), max(a.warmup, 12)
-        dt_s, _, _, _, _ = timed_run(e2, torch, dist, 1, n_s, w_s, a.hash)
+        dt_s, _, _, _, _, _ = timed_run(e2, torch, dist, 1, n_s, w_s, a.hash)
         settle(e2, 50.0, a.hash, 64)
         n2 = max(a.steps, 1024)
-        dt2, kms2, l2, g2, c2 = timed_run(e2, torch, dist, 1, n2, 0, a.hash)
+        dt2, kms2, l2, g2, c2, _ = timed_run(e2, torch, dist, 1, n2, 0, a.hash)
         plan2 = e2.pass_plan(n2, hashes=a.hash)
         # the same board one generation per HBM pass: the pure bandwidth case
         # (north_star: >= 70 % of peak HBM bandwidth at 65536^2)
@@ -312,7 +395,7 @@ def secondary_run(GolEngine, torch, dist, a, local):
         e2.seed(0x5EED)
         settle(e2, 50.0, a.hash, 16)
         n1 = max(a.steps, 256)
-        dt1, kms1, l1, g1, c1 = timed_run(e2, torch, dist, 1, n1, 0, a.hash)
+        dt1, kms1, l1, g1, c1, _ = timed_run(e2, torch, dist, 1, n1, 0, a.hash)
     shape = f"{S}x{S}"
     r2 = roofline(kms2, l2, g2, S * S, plan2, shape, "N1", a.hash, c2)
     r1 = roofline(kms1, l1, g1, S * S, [1] * n1, shape, "N1", a.hash, c1)
@@ -324,7 +407,11 @@ def secondary_run(GolEngine, torch, dist, a, local):
                          "note": "fresh seed right after context creation: inside the clock's recovery"},
         "single_generation_passes": {"value": round(S * S * n1 / dt1 / 1e9, 2), "unit": "GCUPS", "steps": n1,
                                      "warmup": "50 ms settled", "ms_per_step": round(dt1 / n1 * 1e3, 4),
-                                     "roofline": r1}})
+                                     "roofline": r1,
+                                     # the same bytes over the wall-clock time per generation
+                                     # (launch gaps included), beside the kernel-time frac
+                                     "hbm_frac_from_ms_per_step": round(
+                                         S * S * BYTES_PER_CELL_UPDATE / (dt1 / n1) / 1e9 / HBM_PEAK_GBS, 4)}})
     return out
 
 
@@ -343,7 +430,7 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
     eng.comm_init(N.unique_id(), 0, 1)
     eng.seed(0x5EED)
     settle(eng, 50.0, False, 12)
-    dt, kms, launches, gcov, _ = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
+    dt, kms, launches, gcov, _, _ = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
     out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
                                     "warmup": warm, "ms_per_step": round(dt / a.steps * 1e3, 4),
                                     "pass_plan": eng.pass_plan(min(a.steps, 1024))}
@@ -358,7 +445,7 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
         if not a.no_secondary:
             secondary_run(GolEngine, torch, dist, a, local)
         e8.seed(0x5EED)
-        dtf, _, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        dtf, _, _, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         out["per_rank_shard_driver_window"] = {
             "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dtf / 1e9, 2),
             "unit": "GCUPS", "warmup": a.warmup, "ms_per_step": round(dtf / a.steps * 1e3, 4),
@@ -367,7 +454,7 @@ def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
                     "run can reach before any xGMI cost"}
         e8.seed(0x5EED)
         settle(e8, 50.0, False, 12)
-        dt8, kms8, l8, g8, c8 = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+        dt8, kms8, l8, g8, c8, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
         plan8 = e8.pass_plan(min(a.steps, 1024))
     out["per_rank_shard_self_ring"] = {
         "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
@@ -413,23 +500,37 @@ def main():
         if not a.no_secondary:
             secondary = secondary_run(GolEngine, torch, dist, a, local)
             secondary["note"] = f"measured on rank {rank}'s GPU; each of the {world} ranks ran it on its own GPU"
-    eng.seed(0x5EED)
+    eng.seed(GOLDEN_SEED)
+    parity = Parity(W, H)
 
-    dt, kms, launches, gcov, clk = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    dt, kms, launches, gcov, clk, hs = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    e1 = a.warmup + a.steps
+    rank_times = list(getattr(timed_run, "rank_times", []))
+    if hs is not None:
+        parity.sequence("fused per-generation hashes of the W + K generations (global: shard partials "
+                        "summed by gol_comm_allreduce_u64 at N > 1)",
+                        1, eng.allreduce_u64(hs) if world > 1 else hs)
+    parity.board("gol_hash of the board after the W + K generations (summed over the ranks)", e1,
+                 global_hash(eng, world))
     eng_info = {g: eng.occupancy(g) for g in range(1, 13)}
     plan = eng.pass_plan(min(a.steps, 1024), hashes=a.hash)
     value = W * H * a.steps / dt / 1e9
     hashed = None
-    if world == 1 and not a.hash:
+    if not a.hash:
         # the same workload with the fused per-generation state hash (the
         # parity contract's output: one u64 per generation),
-        # continuing from the board the timed run left
-        dth, kmsh, lh, gh, ch = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
+        # continuing from the board the timed run left; at N > 1 the shards'
+        # per-generation partials are summed over the ring (RCCL all-reduce)
+        dth, kmsh, lh, gh, ch, hh = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
+        parity.sequence("fused per-generation hashes of the hashed window (global: shard partials summed "
+                        "by gol_comm_allreduce_u64 at N > 1)", e1 + 1, eng.allreduce_u64(hh) if world > 1 else hh)
+        parity.board("gol_hash of the board after the hashed window", 2 * e1, global_hash(eng, world))
         hplan = eng.pass_plan(min(a.steps, 1024), hashes=True)
         vh = W * H * a.steps / dth / 1e9
         hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
                   "frac_of_unhashed": round(vh / value, 4), "pass_plan": hplan,
-                  "roofline": roofline(kmsh, lh, gh, W * H, hplan, f"{W}x{H}", "N1", True, ch)}
+                  "roofline": roofline(kmsh, lh, gh, W * rows if world == 1 else W * max(rows - round(2 * gh / max(lh, 1)), 0),
+                                       hplan, f"{W}x{rows}", "N1" if world == 1 else "ring", True, ch)}
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
     G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
@@ -464,9 +565,10 @@ def main():
                    "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash)},
         "roofline": roof,
+        "parity": parity.report(),
     }
     if world > 1:
-        rt = timed_run.rank_times
+        rt = rank_times
         out["ranks"] = {"ms_per_step": [round(x / a.steps * 1e3, 4) for x in rt],
                         "rows": [N.shard_rows(H, r, world)[1] for r in range(world)],
                         "gcups": [round(W * N.shard_rows(H, r, world)[1] * a.steps / x / 1e9, 2)

@@ -184,6 +184,14 @@ int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_wo
  * NULL) receives the epoch the copy holds.  GOL_ESTATE if none is in flight. */
 int gol_snapshot_wait(gol_ctx* ctx, uint64_t* epoch_out);
 
+/* Non-blocking: *landed = 1 if the snapshot started by gol_snapshot_async
+ * has reached the host buffer, 0 if it is still in flight (a JVM worker polls
+ * this instead of blocking its actor thread; the fault path asks it of a lost
+ * shard: a checkpoint that had not landed when the backend died never
+ * existed).  GOL_ESTATE if none is in flight.  gol_snapshot_wait still ends
+ * the snapshot. */
+int gol_snapshot_query(gol_ctx* ctx, int* landed);
+
 /* Page-locked host memory for snapshot / load buffers (the JVM side wraps it
  * in a direct ByteBuffer); free with gol_host_free. */
 int gol_host_alloc(size_t bytes, void** out);
@@ -240,6 +248,11 @@ int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count);
 typedef struct gol_group gol_group;
 int gol_group_create(gol_group** out, gol_ctx* const* shards, int n);
 int gol_group_step(gol_group* group, uint32_t generations, uint64_t* hashes_out);
+/* gol_group_step that also returns every shard's per-generation partial
+ * hashes: partials_out[k * generations + g] = shard k's partial of generation
+ * g (hashes_out required).  The fault path keeps them to check a re-spawned
+ * shard's replayed partials against the recorded global hashes. */
+int gol_group_step_partials(gol_group* group, uint32_t generations, uint64_t* hashes_out, uint64_t* partials_out);
 int gol_group_sync(gol_group* group);
 const char* gol_group_last_error(const gol_group* group);
 void gol_group_destroy(gol_group* group);
@@ -282,6 +295,19 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
  * step kernel relies on (DPP wave shifts, v_alignbit, scalar loads) and
  * writes 256 words to report (layout: gol_kernels.hip selftest_kernel). */
 int gol_selftest(int device, uint32_t* report);
+
+/* Diagnostics of the HIP status discipline.  A failing
+ * HIP call leaves its status pending on the calling thread (hipGetLastError);
+ * libgol takes every status it reports or logs off the thread, launches its
+ * kernels with calls that return their own status, and absorbs what RCCL's
+ * own HIP calls leave behind right after each RCCL call.  So after any libgol
+ * entry point the thread has no pending HIP status that libgol produced.
+ *   gol_diag_take_hip_error: the calling thread's pending HIP status (0: none),
+ *                            taken off the thread (hipGetLastError).
+ *   gol_diag_absorbed:       how many statuses RCCL calls left behind, and the
+ *                            last one's description (`last` may be NULL). */
+int gol_diag_take_hip_error(int* code);
+int gol_diag_absorbed(uint64_t* count, char* last, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -10,9 +10,12 @@ CPU ranks: every engine call is appended to $FAKE_LOG_DIR/rank<r>.log.
     RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. FAKE_LOG_DIR=.. \
         python tests/bench_fake_runner.py --gpus N --steps K --warmup W ...
 """
+import json
 import os
 import sys
 import types
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RANK = int(os.environ.get("RANK", "0"))
@@ -24,12 +27,56 @@ def log(*parts):
         f.write(" ".join(str(p) for p in parts) + "\n")
 
 
+M64 = (1 << 64) - 1
+
+
+def golden(width):
+    with open(os.path.join(ROOT, "tests", "golden", f"bench_{width}.json")) as f:
+        return [int(x, 16) for x in json.load(f)["hashes"]]
+
+
 class FakeEngine:
+    """Records calls; its state hash is a share of the golden hash of its
+    epoch: rank r > 0 holds a pseudo-random share, rank 0 the rest, so only
+    the sum over all ranks (the all-reduce) equals the golden value."""
+
     def __init__(self, width, height, topology="torus", rule="life", device=0, row0=0, rows=0):
         self.w, self.h, self.rows = width, height, rows or height
         self.gens = self.launches = 0
         self.ms = 0.0
+        self.epoch = 0
+        self.whole = self.rows == height
         log("create", f"{width}x{self.rows}", "device", device, "row0", row0)
+
+    def _share(self, epoch):
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if self.whole or world == 1:
+            g = golden(self.w)
+            return g[epoch] if epoch < len(g) else 0
+        others = [(0x9E3779B97F4A7C15 * (epoch + 1) * (r + 7)) & M64 for r in range(1, world)]
+        if RANK > 0:
+            # FAKE_CORRUPT_RANK: this rank's shard goes wrong from epoch 20 on
+            # (a halo-exchange bug), which the summed hash must expose
+            bad = os.environ.get("FAKE_CORRUPT_RANK") == str(RANK) and epoch >= 20
+            return (others[RANK - 1] + (1 if bad else 0)) & M64
+        g = golden(self.w)
+        return ((g[epoch] if epoch < len(g) else 0) - sum(others)) & M64
+
+    def hash(self):
+        log("hash", f"{self.w}x{self.rows}", self.epoch)
+        return self._share(self.epoch)
+
+    def allreduce_u64(self, values):
+        import torch
+        import torch.distributed as dist
+        v = np.asarray(values, dtype=np.uint64)
+        lo = torch.tensor((v & np.uint64(0xFFFFFFFF)).astype(np.int64))
+        hi = torch.tensor((v >> np.uint64(32)).astype(np.int64))
+        dist.all_reduce(lo)
+        dist.all_reduce(hi)
+        log("allreduce", len(v))
+        out = [((int(h) << 32) + int(l)) & M64 for l, h in zip(lo.tolist(), hi.tolist())]
+        return np.array(out, dtype=np.uint64)
 
     def __enter__(self):
         return self
@@ -47,6 +94,7 @@ class FakeEngine:
         log("comm_init", uid.hex()[:16], rank, world)
 
     def seed(self, seed):
+        self.epoch = 0
         log("seed", f"{self.w}x{self.rows}")
 
     def pass_plan(self, n, hashes=False):
@@ -59,6 +107,11 @@ class FakeEngine:
         self.launches += len(plan)
         self.ms += 1e-9 * self.w * self.rows * n / 100.0  # 100k GCUPS
         log("step", f"{self.w}x{self.rows}", n, "hashes" if hashes else "")
+        e0 = self.epoch
+        self.epoch += n
+        if hashes:
+            return np.array([self._share(e0 + k + 1) for k in range(n)], dtype=np.uint64)
+        return None
 
     def sync(self):
         pass

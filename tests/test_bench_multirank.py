@@ -21,12 +21,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, tmp_path, *args):
+def _run(world, tmp_path, *args, extra_env=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), FAKE_LOG_DIR=str(tmp_path), OMP_NUM_THREADS="1")
+                   MASTER_PORT=str(port), FAKE_LOG_DIR=str(tmp_path), OMP_NUM_THREADS="1", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, RUNNER, "--gpus", str(world), *args], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=120) for p in procs]
@@ -70,7 +70,32 @@ def test_multirank_bench_line(tmp_path, world):
         # W warm-up then exactly K timed generations on the shard
         shard_steps = [int(ln.split()[2]) for ln in log if ln.startswith(f"step 262144x{rows} ")]
         assert shard_steps[:2] == [5, 20]
+        # then the hashed window (W + K more generations with hashes), and each
+        # rank's shard hash goes through the all-reduce
+        assert [ln.split()[2:] for ln in log if ln.startswith(f"step 262144x{rows} ")][2:4] == \
+            [["5", "hashes"], ["20", "hashes"]]
+        assert [ln.split()[2] for ln in log if ln.startswith(f"hash 262144x{rows}")] == ["25", "50"]
+        assert sum(1 for ln in log if ln.startswith("allreduce")) == 3
     assert len(uids) == 1  # every rank joined rank 0's communicator id
+    # parity vs tests/golden/bench_262144.json: only the sum over the ranks
+    # of the shard hashes equals the golden value
+    par = d["parity"]
+    assert par["match"] is True, par
+    whats = [(c.get("epoch"), c.get("epochs")) for c in par["checks"]]
+    assert whats == [(25, None), (None, [26, 50]), (50, None)]
+    assert par["checks"][1]["checked"] == 25
+
+
+def test_multirank_bench_flags_a_wrong_shard(tmp_path):
+    """A rank whose shard drifts from epoch 20 on (what a broken halo exchange
+    would do) turns parity.match false, and the mismatching epochs are named."""
+    outs, _ = _run(2, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
+                   extra_env={"FAKE_CORRUPT_RANK": "1"})
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    par = d["parity"]
+    assert par["match"] is False
+    assert par["checks"][0]["match"] is False  # epoch 25
+    assert par["checks"][1]["mismatched_epochs"][:2] == [26, 27]
 
 
 def test_single_rank_keeps_cpu_baseline_slot(tmp_path):
@@ -80,6 +105,7 @@ def test_single_rank_keeps_cpu_baseline_slot(tmp_path):
     outs, logs = _run(1, tmp_path, "--steps", "12", "--warmup", "2", "--no-cpu", "--no-ring")
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and "note" not in d["secondary"]
+    assert d["parity"]["match"] is True and d["parity"]["checks"][0]["epoch"] == 14
     log = logs[0]
     i_sec = next(i for i, ln in enumerate(log) if ln.startswith("create 65536x65536"))
     i_main = next(i for i, ln in enumerate(log) if ln.startswith("create 262144x262144"))

@@ -1,8 +1,9 @@
 """bench.py's roofline fields (CPU: pure functions over a synthetic PMC
 table).  The dominant multi-generation kernel is reported against the VALU
-issue ceiling at the PMC-measured clock (frac <= 1 for any rate the model
-allows), with the physical HBM fraction and the 2-bit/cell/generation
-'effective' figure beside it; single-generation passes stay HBM-bound."""
+issue ceiling at the guide's 2.4 GHz max clock (frac <= 1 for any rate the
+model allows); the clock the launches held prices a separate issue-efficiency
+diagnostic; the physical HBM fraction and the 2-bit/cell/generation
+'effective' figure sit beside it; single-generation passes stay HBM-bound."""
 import bench
 
 
@@ -17,23 +18,25 @@ def test_valu_roofline_with_pmc(monkeypatch):
     cells = 262144 * 262144
     r = bench.roofline(kms=13.0, launches=3, gens_covered=20, cells=cells, plan=[6, 6, 8],
                        shape="262144x262144", mode="N1")
-    assert r["bound"] == "valu" and r["unit"] == "GCUPS"
+    assert r["bound"] == "valu" and r["unit"] == "GCUPS" and r["peak_clock_ghz"] == 2.4
     clock = (2.0 * 4 + 2.0 * 4 + 1.9 * 5) / 13
-    assert abs(r["clock_ghz"] - round(clock, 3)) < 1e-3
-    peak = 1024 * clock * 2048 / 29.1
+    assert abs(r["held_clock"]["clock_pmc_ghz"] - round(clock, 3)) < 1e-3
+    peak = 1024 * 2.4 * 2048 / 29.1  # the guide's max clock, whatever the launches held
     achieved = cells * 20 / 3 / (13.0 / 3 / 1e3) / 1e9
     assert abs(r["peak"] - peak) < 1.0 and abs(r["achieved"] - achieved) < 1.0
     assert abs(r["frac"] - achieved / peak) < 1e-3 and r["frac"] < 1
+    assert "issue_efficiency" not in r["held_clock"]  # no probe clock given
     assert r["traffic"] == 18e9
     assert r["hbm"]["frac"] < 1 and r["hbm_effective"]["frac"] > 1
 
 
-def test_missing_pmc_entry_falls_back_to_max_clock(monkeypatch):
+def test_missing_pmc_entry(monkeypatch):
     _table(monkeypatch, {})
     r = bench.roofline(kms=10.0, launches=2, gens_covered=16, cells=1 << 30, plan=[8, 8],
                        shape="65536x16384", mode="ring")
-    assert r["traffic"] is None and r["clock_ghz"] == bench.CLOCK_MAX_GHZ
-    assert r["frac"] == r["frac_at_max_clock"] and "hbm" not in r
+    assert r["traffic"] is None and r["held_clock"]["clock_pmc_ghz"] is None and "hbm" not in r
+    peak, _ = bench.valu_peak_gcups(bench.VALU_MIX, bench.CLOCK_MAX_GHZ)
+    assert abs(r["peak"] - round(peak, 1)) < 0.2
 
 
 def test_single_generation_passes_are_hbm_bound(monkeypatch):
@@ -56,14 +59,19 @@ def test_compact_plan_keeps_json_short():
     assert bench.compact_plan([12] * 7 + [9, 9]) == "7 x 12 + 2 x 9"
 
 
-def test_live_probe_clock_takes_precedence(monkeypatch):
+def test_probe_clock_prices_only_the_issue_efficiency(monkeypatch):
     """The clock measured inside the timed launches (gol_profile_clock) prices
-    the VALU ceiling; the PMC table's clock stays beside it."""
+    held_clock.issue_efficiency; frac stays priced at 2.4 GHz."""
     ent = {"launch_ms": 4.0, "hbm_bytes": 18e9, "clock_ghz": 2.2, "valu_per_word_gen": 12.0,
            "generations_per_launch": 12}
     _table(monkeypatch, {"262144x262144/N1/G12/h0": ent})
     r = bench.roofline(kms=12.0, launches=2, gens_covered=24, cells=262144 * 262144, plan=[12, 12],
                        shape="262144x262144", mode="N1", clock=1.9)
-    assert r["clock_ghz"] == 1.9 and "probe" in r["clock_source"] and r["clock_pmc_ghz"] == 2.2
-    peak, _ = bench.valu_peak_gcups(bench.VALU_MIX, 1.9)
-    assert abs(r["peak"] - round(peak, 1)) < 0.2 and r["traffic"] == 18e9
+    hc = r["held_clock"]
+    assert hc["ghz"] == 1.9 and "probe" in hc["source"] and hc["clock_pmc_ghz"] == 2.2
+    peak_held, _ = bench.valu_peak_gcups(bench.VALU_MIX, 1.9)
+    peak_max, _ = bench.valu_peak_gcups(bench.VALU_MIX, 2.4)
+    assert abs(hc["peak_at_held_clock"] - round(peak_held, 1)) < 0.2
+    assert abs(r["peak"] - round(peak_max, 1)) < 0.2
+    assert abs(hc["issue_efficiency"] * peak_held - r["frac"] * peak_max) < 5
+    assert r["frac"] < hc["issue_efficiency"] and r["traffic"] == 18e9

@@ -166,3 +166,49 @@ def test_recurring_crashes_async_checkpoints(gpu):
     final, want = O.run_packed(O.seed_packed(W, H, 0x5EED), W, gens, O.TORUS, O.LIFE)
     assert got == [int(x) for x in want]
     assert (board == final).all()
+
+
+@pytest.mark.parametrize("landed", [False, True])
+def test_kill_while_async_checkpoint_in_flight(gpu, landed):
+    """a shard lost while its background checkpoint is in flight.
+    If its part had not landed, the whole set is dropped and recovery replays
+    from the previous committed checkpoint (a longer light cone); if it had,
+    the set is the recovery point.  Either way every hash equals the oracle's,
+    and the replayed partials complete the recorded global hashes."""
+    from gameoflife import _native as N
+    from gameoflife.fault import ShardedSimulation
+    W, H, gens = 32 * 100, 80, 40
+    sim = ShardedSimulation(W, H, 8, list(range(N.device_count())), checkpoint_every=10, async_checkpoints=True)
+    got = sim.step(20)              # the epoch-20 checkpoint is now in flight
+    sim.kill(3, checkpoint_landed=landed)
+    replayed = sim.respawn(3)
+    c = 20 if landed else 10
+    assert f"respawn shard 3 on device {sim.placement[3]}, light cone {c}->20" in sim.events
+    assert len(replayed) == 20 - c
+    assert any("dropped" in e for e in sim.events) != landed
+    got += sim.step(gens - 20)
+    board = sim.snapshot()
+    sim.close()
+    final, want = O.run_packed(O.seed_packed(W, H, 0x5EED), W, gens, O.TORUS, O.LIFE)
+    assert got == [int(x) for x in want]
+    assert (board == final).all()
+
+
+def test_snapshot_query_reports_landing(gpu):
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    with GolEngine(32 * 64, 64) as e:
+        e.seed(5)
+        with pytest.raises(N.GolError):
+            e.snapshot_landed()  # nothing in flight
+        buf = e.host_buffer()
+        e.snapshot_async(buf)
+        e.sync()
+        import time
+        t0 = time.time()
+        while not e.snapshot_landed() and time.time() - t0 < 10:
+            time.sleep(0.001)
+        assert e.snapshot_landed()
+        assert e.snapshot_wait() == 0
+        assert (buf == O.seed_packed(32 * 64, 64, 5)).all()
+

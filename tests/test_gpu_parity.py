@@ -50,6 +50,25 @@ def check_run(W, H, gens, rule=O.LIFE, topology="torus", seed=None, cells=None, 
     np.testing.assert_array_equal(final_gpu, final_cpu)
 
 
+def check_run_unhashed_g1(W, H, gens, rule=O.LIFE, topology="torus", seed=0, vec=0, band=0, cells=None):
+    """One generation per pass without the fused hash -- step_kernel<VEC, ...,
+    HASH=false> with its non-temporal stores, the kernel behind bench.py's
+    single_generation_passes line -- checked by the final board word for word
+    and gol_hash against the oracle's last per-generation hash."""
+    topo = O.TORUS if topology == "torus" else O.REF_CLIPPED
+    board = O.pack(cells) if cells is not None else O.seed_packed(W, H, seed)
+    with engine(W, H, topology=topology, rule=rule_obj(rule)) as e:
+        e.set_tuning(band_rows=band, gens_per_pass=1, words_per_lane=vec)
+        assert e.pass_plan(gens) == [1] * gens
+        e.load(board)
+        e.step(gens)
+        h = e.hash()
+        final_gpu = e.snapshot()
+    final_cpu, want = O.run_packed(board, W, gens, topo, rule)
+    np.testing.assert_array_equal(final_gpu, final_cpu)
+    assert h == int(want[-1])
+
+
 def test_selftest_cross_lane(gpu):
     from gameoflife.engine import selftest
     rep = selftest(gpu)
@@ -127,6 +146,25 @@ def test_words_per_lane(gpu, vec, gpp):
     rng = np.random.default_rng(vec * 10 + gpp)
     cells = (rng.random((31, 32 * 132 - 9)) < 0.5).astype(np.uint8)
     check_run(32 * 132 - 9, 31, 9, O.LIFE, "ref-clipped", cells=cells, gpp=gpp, vec=vec)
+
+
+@pytest.mark.parametrize("vec", [1, 2, 4])
+@pytest.mark.parametrize("W,H", TORUS_SHAPES)
+def test_unhashed_single_generation_torus(gpu, W, H, vec):
+    # every lane width; full and partial strips (e.g. 130 words = 2 strips of
+    # 64 x 2 words, the second with one lane), a single word, many strips
+    if (W // 32) % vec:
+        pytest.skip("words per lane must divide the row")
+    check_run_unhashed_g1(W, H, 5, seed=W + H + vec, vec=vec)
+
+
+@pytest.mark.parametrize("band", [1, 3, 4, 16, 0])
+def test_unhashed_single_generation_bands_rules_clipped(gpu, band):
+    check_run_unhashed_g1(32 * 520, 37, 4, seed=band, band=band)
+    check_run_unhashed_g1(32 * 12, 29, 4, rule=(0x0C8, 0x1A6), seed=band, band=band)
+    rng = np.random.default_rng(band)
+    cells = (rng.random((31, 32 * 132 - 9)) < 0.5).astype(np.uint8)
+    check_run_unhashed_g1(32 * 132 - 9, 31, 4, topology="ref-clipped", cells=cells, band=band)
 
 
 def test_tuning_rejects_bad_values(gpu):
