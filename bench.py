@@ -235,11 +235,34 @@ def cpu_baseline(width, seconds):
            "threads_source": "OMP_NUM_THREADS (the job's CPU share)" if share > 0 else "sched_getaffinity",
            "sample": f"oracle_run_packed (oracle/gol_oracle.c, bit-sliced, OpenMP), {width}x{H} torus B3/S23 "
                      f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
+    quota = cgroup_cpus()
+    if quota:
+        out["cgroup_cpu_quota"] = quota
     if affinity > threads:
         va, ga, dta = _cpu_rate(O, width, H, affinity, max(seconds / 3, 1.0))
         out["all_affinity"] = {"value": round(va, 3), "unit": "GCUPS", "cores": affinity,
-                               "sample": f"same slice, {ga} generations in {dta:.1f} s on {affinity} threads"}
+                               "sample": f"same slice, {ga} generations in {dta:.1f} s on {affinity} threads",
+                               "note": (f"the job's cgroup grants {quota:g} CPUs: {affinity} threads time-slice on "
+                                        "them" if quota and quota < affinity else "every core of sched_getaffinity")}
     return out
+
+
+def cgroup_cpus():
+    """CPUs the job's cgroup (v2 cpu.max, else v1 cfs quota) allows, or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
 
 
 def pmc_launch():
