@@ -375,6 +375,24 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
     // the plain choice (137 rows, no tail) and 0.0471 for 256 rows without
     // the tail; at G = 6 the plain choice stays best.
     if (strips < 32 && gens >= 7 && resident > 0) return (int)std::min<int64_t>(256, std::max<int64_t>(rows, 1));
+    // Wide boards at 7- to 12-generation passes, when the pass is many rounds
+    // of resident waves: the tallest band (up to 1024 rows at G >= 10, 768
+    // below) that still leaves >= 3.5 rounds, the tail split evening out the
+    // end.  A band of B rows recomputes ~(G - 1) / B of its stage rows as
+    // halo, so taller bands issue fewer VALU per cell.  Same-box sweep on the
+    // bench's window (profiles/r03_band_262144.txt, 5 rounds, 262144^2,
+    // passes 12 + 8): 1024 + 768 116.1k, 768 + 512 115.9k, 576 + 384 115.5k,
+    // the previous 384 + ~256 114.4k GCUPS; on the N = 8 per-rank shape
+    // (262144 x 32768, < 2 rounds) taller bands lost up to 6 %
+    // (profiles/r03_band_32768.txt), so it keeps the rules below.
+    if (strips >= 32 && gens >= 7 && resident > 0) {
+        const int cap = gens >= 10 ? 1024 : 768;
+        for (const int b : {1024, 768, 512}) {
+            if (b > cap) continue;
+            const int64_t waves = (rows + b - 1) / b * strips;
+            if (2 * waves >= 7 * resident) return (int)std::min<int64_t>(b, std::max<int64_t>(rows, 1));
+        }
+    }
     // Wide boards at 10- to 12-generation passes (3 waves per SIMD, 2G halo
     // rows per band): 384-row bands when that is still >= 3 rounds of
     // resident waves, else 256, both with the tail split.  Same-box sweep at

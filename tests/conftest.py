@@ -43,3 +43,15 @@ def gpu():
     if not _gpu_available():
         pytest.fail("no HIP device: -m gpu tests need an MI355X")
     return 0
+
+
+def pytest_terminal_summary(terminalreporter):
+    """GPU runs: how many HIP statuses RCCL calls left behind during the
+    session (libgol absorbs and counts them)."""
+    mod = sys.modules.get("gameoflife._native")
+    if mod is None or not _gpu_available():
+        return
+    n, last = mod.absorbed()
+    terminalreporter.write_line(f"libgol: HIP statuses absorbed after RCCL calls this session: {n}"
+                                + (f" (last: {last})" if n else ""))
+
