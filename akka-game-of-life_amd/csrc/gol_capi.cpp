@@ -14,7 +14,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <functional>
+#include <memory>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -48,6 +52,8 @@ struct gol_group {
     bool torus = true;
     std::string err;
 };
+
+struct LoopRing;
 
 struct gol_ctx {
     // geometry
@@ -84,6 +90,9 @@ struct gol_ctx {
     // RCCL
     ncclComm_t nccl = nullptr;
     int rank = 0, nranks = 1;
+    // loopback ring (gol_comm_init_loopback): the same halo exchange between
+    // contexts of one process, for tests; exclusive with nccl
+    std::shared_ptr<LoopRing> loop;
     // in-process shard group (gol_group_*): halos by device-to-device copies
     gol_group* group = nullptr;
     int gindex = 0;
@@ -184,8 +193,10 @@ size_t group_size(const gol_group* g);
 // and come back through ncclSend / ncclRecv to self (the "self-ring" -- the
 // RCCL path exercised bit-exactly on a one-GPU box).
 bool sharded(const gol_ctx* c) {
-    return c->nccl != nullptr || (c->group != nullptr && group_size(c->group) > 1);
+    return c->nccl != nullptr || c->loop != nullptr || (c->group != nullptr && group_size(c->group) > 1);
 }
+
+bool in_ring(const gol_ctx* c) { return c->nccl != nullptr || c->loop != nullptr; }
 
 int bind(gol_ctx* ctx) {
     HIP_CHECK(ctx, hipSetDevice(ctx->device));
@@ -609,6 +620,149 @@ int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool ha
     return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
 }
 
+// One point-to-point operation of a pass's halo exchange: send `count`
+// words from `buf` to rank `peer`, or receive them into `buf` from it.
+struct HaloOp {
+    bool send;
+    uint32_t* buf;
+    size_t count;
+    int peer;
+};
+
+}  // namespace
+
+// Loopback ring (gol_comm_init_loopback): contexts of one process -- one host
+// thread each, like one process per GPU -- joined under a key run libgol's
+// exact halo op list with ncclSend / ncclRecv semantics: operations between a
+// (sender, receiver) pair match in FIFO order of issue, and a rank's group
+// completes when all its operations have matched.  A matched pair is a
+// device-to-device copy on the receiver's comm stream, ordered after the
+// sender's plane was final (an event on the sender's comm stream) and before
+// the sender's stream goes on (an event the sender's comm stream waits for),
+// as an RCCL send / recv pair is.  Test transport: the product path is RCCL.
+struct LoopRing {
+    std::mutex mu;
+    std::condition_variable cv;
+    int nranks = 0;
+    int joined = 0;
+    struct Op {
+        gol_ctx* ctx;
+        uint32_t* buf;
+        size_t bytes;
+        hipEvent_t ready = nullptr;  // sends: the data is final on the sender's comm stream
+        bool matched = false;
+        int err = GOL_OK;
+    };
+    std::map<std::pair<int, int>, std::deque<std::shared_ptr<Op>>> sends, recvs;  // key (src, dst)
+    std::vector<uint64_t> acc, result;
+    int arrived = 0;
+    uint64_t round = 0;
+};
+
+namespace {
+
+std::mutex g_loop_mu;
+std::map<std::string, std::weak_ptr<LoopRing>> g_loops;
+
+// Match the queued sends src -> dst with the receives posted for them (ring
+// lock held): FIFO per pair, like NCCL point-to-point.
+void loop_match(LoopRing& ring, int src, int dst) {
+    auto& sq = ring.sends[{src, dst}];
+    auto& rq = ring.recvs[{src, dst}];
+    while (!sq.empty() && !rq.empty()) {
+        auto snd = sq.front(), rcv = rq.front();
+        sq.pop_front();
+        rq.pop_front();
+        hipError_t e = hipSuccess;
+        if (snd->bytes != rcv->bytes) {
+            snd->err = rcv->err = GOL_ECOMM;
+        } else {
+            hipEvent_t done = nullptr;
+            e = hipSetDevice(rcv->ctx->device);
+            if (e == hipSuccess) e = hipStreamWaitEvent(rcv->ctx->comm, snd->ready, 0);
+            if (e == hipSuccess)
+                e = hipMemcpyPeerAsync(rcv->buf, rcv->ctx->device, snd->buf, snd->ctx->device, snd->bytes,
+                                       rcv->ctx->comm);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(done, rcv->ctx->comm);
+            if (e == hipSuccess) e = hipSetDevice(snd->ctx->device);
+            if (e == hipSuccess) e = hipStreamWaitEvent(snd->ctx->comm, done, 0);
+            if (done) hip_note(hipEventDestroy(done), "loopback: hipEventDestroy");
+            if (e != hipSuccess) {
+                hip_note(e, "loopback: halo copy");
+                snd->err = rcv->err = GOL_EHIP;
+            }
+        }
+        snd->matched = rcv->matched = true;
+    }
+}
+
+int loop_exchange(gol_ctx* ctx, const HaloOp* ops, int n) {
+    LoopRing& ring = *ctx->loop;
+    std::vector<std::shared_ptr<LoopRing::Op>> mine;
+    {
+        std::unique_lock<std::mutex> lk(ring.mu);
+        for (int k = 0; k < n; ++k) {
+            auto op = std::make_shared<LoopRing::Op>();
+            op->ctx = ctx;
+            op->buf = ops[k].buf;
+            op->bytes = ops[k].count * sizeof(uint32_t);
+            if (ops[k].send) {
+                HIP_CHECK(ctx, hipEventCreateWithFlags(&op->ready, hipEventDisableTiming));
+                HIP_CHECK(ctx, hipEventRecord(op->ready, ctx->comm));
+                ring.sends[{ctx->rank, ops[k].peer}].push_back(op);
+                loop_match(ring, ctx->rank, ops[k].peer);
+            } else {
+                ring.recvs[{ops[k].peer, ctx->rank}].push_back(op);
+                loop_match(ring, ops[k].peer, ctx->rank);
+            }
+            mine.push_back(op);
+        }
+        ring.cv.notify_all();
+        const bool ok = ring.cv.wait_for(lk, std::chrono::seconds(120), [&] {
+            return std::all_of(mine.begin(), mine.end(), [](const auto& o) { return o->matched; });
+        });
+        if (!ok) return set_err(ctx, GOL_ECOMM, "loopback ring: a peer never posted its halo operations");
+    }
+    int rc = bind(ctx);  // a match made on this thread may have switched devices
+    for (auto& op : mine) {
+        if (op->ready) hip_note(hipEventDestroy(op->ready), "loopback: hipEventDestroy");
+        if (op->err && !rc) rc = set_err(ctx, op->err, "loopback ring: halo operation failed");
+    }
+    return rc;
+}
+
+int loop_allreduce(gol_ctx* ctx, uint64_t* values, uint32_t count) {
+    LoopRing& ring = *ctx->loop;
+    std::unique_lock<std::mutex> lk(ring.mu);
+    if (ring.arrived == 0) ring.acc.assign(values, values + count);
+    else if (ring.acc.size() != count) return set_err(ctx, GOL_EINVAL, "loopback all-reduce: counts differ");
+    else for (uint32_t k = 0; k < count; ++k) ring.acc[k] += values[k];
+    const uint64_t my_round = ring.round;
+    if (++ring.arrived == ring.nranks) {
+        ring.result = ring.acc;
+        ring.arrived = 0;
+        ++ring.round;
+        ring.cv.notify_all();
+    } else if (!ring.cv.wait_for(lk, std::chrono::seconds(120), [&] { return ring.round != my_round; })) {
+        return set_err(ctx, GOL_ECOMM, "loopback all-reduce: a peer never joined");
+    }
+    std::copy(ring.result.begin(), ring.result.end(), values);
+    return GOL_OK;
+}
+
+void loop_leave(gol_ctx* ctx) {
+    if (!ctx->loop) return;
+    std::lock_guard<std::mutex> lk(g_loop_mu);
+    {
+        std::lock_guard<std::mutex> rl(ctx->loop->mu);
+        --ctx->loop->joined;
+    }
+    ctx->loop.reset();
+    for (auto it = g_loops.begin(); it != g_loops.end();)
+        it = it->second.expired() ? g_loops.erase(it) : std::next(it);
+}
+
 // One pass of G generations (temporal blocking, G <= kMaxGensPerPass) of a
 // stand-alone or RCCL-sharded context.  slots: the hash accumulators of these
 // G generations (G * kHashGenStride), or null.
@@ -634,17 +788,29 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
         const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
-        NCCL_CHECK(ctx, ncclGroupStart());
         // Issue order matters when up == down (2 ranks, or 1 rank sending to
         // itself): per-peer FIFO matching pairs my last rows with the peer's
         // top halo and my first rows with its bottom halo
-        // (gameoflife/shard.py HaloPlan mirrors this order).
-        if (has_down)
-            NCCL_CHECK(ctx, ncclSend(cur + (int64_t)(rows - G) * pitch, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
-        if (has_up) NCCL_CHECK(ctx, ncclSend(cur, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
-        if (has_up) NCCL_CHECK(ctx, ncclRecv(ctx->halo_top, cnt, ncclUint32, up, ctx->nccl, ctx->comm));
-        if (has_down) NCCL_CHECK(ctx, ncclRecv(ctx->halo_bot, cnt, ncclUint32, down, ctx->nccl, ctx->comm));
-        NCCL_CHECK(ctx, ncclGroupEnd());
+        // (gameoflife/shard.py HaloPlan mirrors this order).  One op list,
+        // run by RCCL or by the in-process loopback ring.
+        HaloOp ops[4];
+        int nops = 0;
+        if (has_down) ops[nops++] = {true, cur + (int64_t)(rows - G) * pitch, cnt, down};
+        if (has_up) ops[nops++] = {true, cur, cnt, up};
+        if (has_up) ops[nops++] = {false, ctx->halo_top, cnt, up};
+        if (has_down) ops[nops++] = {false, ctx->halo_bot, cnt, down};
+        if (ctx->loop) {
+            if (int rc = loop_exchange(ctx, ops, nops)) return rc;
+        } else {
+            NCCL_CHECK(ctx, ncclGroupStart());
+            for (int k = 0; k < nops; ++k) {
+                if (ops[k].send)
+                    NCCL_CHECK(ctx, ncclSend(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
+                else
+                    NCCL_CHECK(ctx, ncclRecv(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
+            }
+            NCCL_CHECK(ctx, ncclGroupEnd());
+        }
         // The event covers the sends too: the next pass overwrites this plane
         // only after the boundary kernels, which wait for it.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
@@ -741,7 +907,7 @@ int depth_cap(const gol_ctx* ctx) {
     int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass
                                        : (life_torus ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
-    if (ctx->nccl) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
+    if (in_ring(ctx)) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return (int)std::max<int64_t>(G, 1);
 }
@@ -820,6 +986,7 @@ void destroy_impl(gol_ctx* c) {
     hip_note(hipSetDevice(c->device), "destroy: hipSetDevice");
     for (hipStream_t st : {c->compute, c->comm, c->edge, c->xfer})
         if (st) hip_note(hipStreamSynchronize(st), "destroy: hipStreamSynchronize");
+    loop_leave(c);
     if (c->nccl) {
         const ncclResult_t r = ncclCommDestroy(c->nccl);
         absorb_rccl_status("ncclCommDestroy");
@@ -1087,7 +1254,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     if (host_pitch_words < ctx->wwords)
         return set_err(ctx, GOL_EINVAL, "host pitch %lld < words per row %d", (long long)host_pitch_words,
                        ctx->wwords);
-    if (ctx->group || ctx->nccl)
+    if (ctx->group || in_ring(ctx))
         return set_err(ctx, GOL_ESTATE, "replay a shard before it joins its group or ring");
     const int64_t n = generations;
     const int64_t ext = ctx->rows + 2 * n;
@@ -1174,6 +1341,14 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
 
 int gol_comm_abort(gol_ctx* ctx) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
+    if (ctx->loop) {
+        if (int rc = bind(ctx)) return rc;
+        HIP_CHECK(ctx, hipStreamSynchronize(ctx->comm));
+        loop_leave(ctx);
+        ctx->rank = 0;
+        ctx->nranks = 1;
+        return GOL_OK;
+    }
     if (!ctx->nccl) return GOL_OK;
     if (int rc = bind(ctx)) return rc;
     NCCL_CHECK(ctx, ncclCommAbort(ctx->nccl));
@@ -1409,7 +1584,7 @@ int gol_comm_unique_id(uint8_t id_out[GOL_UNIQUE_ID_BYTES]) {
 int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank, int nranks) {
     if (!ctx || !id) return set_err(ctx, GOL_EINVAL, "null argument");
     if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, GOL_EINVAL, "bad rank/nranks");
-    if (ctx->nccl) return set_err(ctx, GOL_ESTATE, "communicator already initialised");
+    if (in_ring(ctx)) return set_err(ctx, GOL_ESTATE, "communicator already initialised");
     if (int rc = bind(ctx)) return rc;
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof uid);
@@ -1419,10 +1594,33 @@ int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank,
     return GOL_OK;
 }
 
+int gol_comm_init_loopback(gol_ctx* ctx, const char* key, int rank, int nranks) {
+    if (!ctx || !key) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (nranks < 1 || rank < 0 || rank >= nranks) return set_err(ctx, GOL_EINVAL, "bad rank/nranks");
+    if (in_ring(ctx)) return set_err(ctx, GOL_ESTATE, "communicator already initialised");
+    if (ctx->group) return set_err(ctx, GOL_ESTATE, "context belongs to a shard group");
+    std::lock_guard<std::mutex> lk(g_loop_mu);
+    std::shared_ptr<LoopRing> ring = g_loops[key].lock();
+    if (!ring) {
+        ring = std::make_shared<LoopRing>();
+        ring->nranks = nranks;
+        g_loops[key] = ring;
+    }
+    std::lock_guard<std::mutex> rl(ring->mu);
+    if (ring->nranks != nranks) return set_err(ctx, GOL_EINVAL, "loopback ring %s has %d ranks", key, ring->nranks);
+    if (ring->joined >= nranks) return set_err(ctx, GOL_ESTATE, "loopback ring %s is full", key);
+    ++ring->joined;
+    ctx->loop = ring;
+    ctx->rank = rank;
+    ctx->nranks = nranks;
+    return GOL_OK;
+}
+
 int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count) {
     if (!ctx || (!values && count)) return set_err(ctx, GOL_EINVAL, "null argument");
-    if (!ctx->nccl) return set_err(ctx, GOL_ECOMM, "no communicator (call gol_comm_init)");
+    if (!in_ring(ctx)) return set_err(ctx, GOL_ECOMM, "no communicator (call gol_comm_init)");
     if (count == 0) return GOL_OK;
+    if (ctx->loop) return loop_allreduce(ctx, values, count);
     if (int rc = bind(ctx)) return rc;
     uint64_t* d = nullptr;
     HIP_CHECK(ctx, hipMallocAsync((void**)&d, count * sizeof(uint64_t), ctx->comm));
@@ -1552,7 +1750,7 @@ int gol_group_create(gol_group** out, gol_ctx* const* shards, int n) {
     for (int k = 0; k < n; ++k) {
         const gol_ctx* s = shards[k];
         if (!s) return set_err(nullptr, GOL_EINVAL, "shard %d is null", k);
-        if (s->group || s->nccl)
+        if (s->group || in_ring(s))
             return set_err(nullptr, GOL_ESTATE, "shard %d already belongs to a group or an RCCL ring", k);
         if (s->width != a->width || s->height != a->height || s->topology != a->topology ||
             s->birth != a->birth || s->survive != a->survive || s->vis_w != a->vis_w || s->vis_h != a->vis_h)

@@ -92,6 +92,7 @@ _SIGNATURES = {
     "gol_comm_init": (_c.c_int, [_vp, _u8p, _c.c_int, _c.c_int]),
     "gol_comm_allreduce_u64": (_c.c_int, [_vp, _u64p, _c.c_uint32]),
     "gol_comm_abort": (_c.c_int, [_vp]),
+    "gol_comm_init_loopback": (_c.c_int, [_vp, _c.c_char_p, _c.c_int, _c.c_int]),
     "gol_replay": (_c.c_int, [_vp, _c.c_uint32, _u32p, _u32p, _c.c_int64, _u64p]),
     "gol_profile_enable": (_c.c_int, [_vp, _c.c_int]),
     "gol_profile_read": (_c.c_int, [_vp, ctypes.POINTER(_c.c_double), _u64p, _u64p]),

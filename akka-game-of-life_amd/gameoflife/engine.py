@@ -173,6 +173,12 @@ class GolEngine:
         arr = (ctypes.c_uint8 * N.GOL_UNIQUE_ID_BYTES).from_buffer_copy(uid)
         self._chk(N.lib.gol_comm_init(self._h, arr, rank, nranks))
 
+    def comm_init_loopback(self, key: str, rank: int, nranks: int) -> None:
+        """Join the in-process loopback ring `key` (gol_comm_init_loopback, a
+        test transport running the RCCL schedule's exact halo operations
+        between contexts of this process, one thread each)."""
+        self._chk(N.lib.gol_comm_init_loopback(self._h, key.encode(), rank, nranks))
+
     def comm_abort(self) -> None:
         """Leave the ring (gol_comm_abort); comm_init may join a new one."""
         self._chk(N.lib.gol_comm_abort(self._h))

@@ -232,6 +232,16 @@ int gol_comm_init(gol_ctx* ctx, const uint8_t id[GOL_UNIQUE_ID_BYTES], int rank,
  * the ring around it (gameoflife/elastic.py). */
 int gol_comm_abort(gol_ctx* ctx);
 
+/* Test transport: join the in-process loopback ring `key` as rank/nranks
+ * instead of an RCCL communicator.  Contexts of one process -- one host
+ * thread each, as one process per GPU would be -- then run exactly the halo
+ * exchange gol_step issues over RCCL (the same send / receive list in the
+ * same order, matched per (sender, receiver) pair in FIFO order like
+ * ncclSend / ncclRecv) as device copies, and gol_comm_allreduce_u64 sums over
+ * them.  This runs the multi-rank schedule with several ranks on one GPU,
+ * where RCCL refuses a second rank.  gol_comm_abort leaves the ring. */
+int gol_comm_init_loopback(gol_ctx* ctx, const char* key, int rank, int nranks);
+
 /* Sum-reduce `count` uint64 values (mod 2^64) across the communicator in
  * place (the per-generation hash reduction). */
 int gol_comm_allreduce_u64(gol_ctx* ctx, uint64_t* values, uint32_t count);
