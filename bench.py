@@ -133,13 +133,17 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
 GOLDEN_SEED = 0x5EED
 
 
+def golden_path(W):
+    return os.path.join("tests", "golden", f"bench_{W}.json")
+
+
 def golden_hashes(W, H):
     """Global state hashes of the bench board (W x H torus, B3/S23, seed
     0x5EED) at epochs 0, 1, ..., from tests/golden/bench_<W>.json -- written by
     tests/golden/make_bench_golden.py with the CPU oracle (a data file: bench
     never runs the oracle to check itself).  None if there is no table."""
     try:
-        with open(os.path.join(ROOT, "tests", "golden", f"bench_{W}.json")) as f:
+        with open(os.path.join(ROOT, golden_path(W))) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
@@ -167,6 +171,7 @@ class Parity:
 
     def __init__(self, W, H):
         self.golden = golden_hashes(W, H)
+        self.source = golden_path(W)
         self.checks = []
 
     def _golden(self, epoch):
@@ -189,7 +194,7 @@ class Parity:
 
     def report(self):
         ms = [c["match"] for c in self.checks]
-        return {"golden": "tests/golden/bench_262144.json (CPU oracle, tests/golden/make_bench_golden.py; "
+        return {"golden": f"{self.source} (CPU oracle, tests/golden/make_bench_golden.py; "
                           "parity unpinned: the reference ships no vectors)" if self.golden else None,
                 "checks": self.checks,
                 "match": None if not ms or any(m is None for m in ms) else all(ms)}

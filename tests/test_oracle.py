@@ -210,3 +210,25 @@ def test_golden_torus_4096_first_generations():
     assert O.hash_packed(b, 4096) == g["hash0"]
     _, hashes = O.run_packed(b, 4096, 20, O.TORUS, O.LIFE)
     assert [int(x) for x in hashes] == g["hashes"][:20]
+
+
+def test_bench_golden_table_epoch0_and_shape():
+    """tests/golden/bench_262144.json (bench.py's parity table): epoch 0 is
+    the oracle's hash of the seed-0x5EED 262144^2 board, recomputed here in
+    row blocks (the hash is a sum over rows, the seed a function of the word
+    index); epochs 1..140 come from make_bench_golden.py's oracle run and are
+    checked on the GPU (the loopback N = 8 ring, config 5 at full size)."""
+    import json
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bench_262144.json")
+    with open(path) as f:
+        d = json.load(f)
+    assert d["board"] == [262144, 262144] and d["seed"] == 0x5EED and d["rule"] == "B3/S23"
+    hashes = [int(x, 16) for x in d["hashes"]]
+    assert len(hashes) == 141 and len(set(hashes)) == 141
+    W = H = 262144
+    total, block = 0, 2048
+    for r0 in range(0, H, block):
+        blk = O.seed_packed(W, H, 0x5EED, row0=r0, rows=block)
+        total = (total + O.hash_packed(blk, W, row0=r0)) % (1 << 64)
+    assert total == hashes[0]
+
