@@ -45,12 +45,18 @@ def main():
     ap.add_argument("--shape", default="262144x262144")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--hash", action="store_true", help="fused per-generation hashes")
+    ap.add_argument("--ring", action="store_true",
+                    help="WxH is one rank's shard of a W x W board, stepped as a 1-rank RCCL self-ring")
     ap.add_argument("configs", nargs="+")
     a = ap.parse_args()
     W, H = (int(x) for x in a.shape.split("x"))
     cfgs = {c: [tuple(int(v) for v in p.split(":")) for p in c.split(",")] for c in a.configs}
     res = {c: [] for c in cfgs}
-    with GolEngine(W, H) as e:
+    eng = GolEngine(W, W, row0=0, rows=H) if a.ring else GolEngine(W, H)
+    if a.ring:
+        from gameoflife import _native as N
+        eng.comm_init(N.unique_id(), 0, 1)
+    with eng as e:
         for passes in cfgs.values():  # load every instance once
             run(e, passes, a.hash)
         for r in range(a.rounds):
