@@ -700,23 +700,34 @@ void loop_match(LoopRing& ring, int src, int dst) {
 int loop_exchange(gol_ctx* ctx, const HaloOp* ops, int n) {
     LoopRing& ring = *ctx->loop;
     std::vector<std::shared_ptr<LoopRing::Op>> mine;
+    // Every send's event is created and recorded before any operation is
+    // posted, so a failure here leaves nothing in the ring for a peer to match.
+    for (int k = 0; k < n; ++k) {
+        auto op = std::make_shared<LoopRing::Op>();
+        op->ctx = ctx;
+        op->buf = ops[k].buf;
+        op->bytes = ops[k].count * sizeof(uint32_t);
+        mine.push_back(op);
+        if (!ops[k].send) continue;
+        hipError_t e = hipEventCreateWithFlags(&op->ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(op->ready, ctx->comm);
+        if (e != hipSuccess) {
+            for (auto& o : mine)
+                if (o->ready) hip_note(hipEventDestroy(o->ready), "loopback: hipEventDestroy");
+            return hip_fail(ctx, e, "loopback: send event", __FILE__, __LINE__);
+        }
+    }
     {
         std::unique_lock<std::mutex> lk(ring.mu);
         for (int k = 0; k < n; ++k) {
-            auto op = std::make_shared<LoopRing::Op>();
-            op->ctx = ctx;
-            op->buf = ops[k].buf;
-            op->bytes = ops[k].count * sizeof(uint32_t);
+            auto& op = mine[k];
             if (ops[k].send) {
-                HIP_CHECK(ctx, hipEventCreateWithFlags(&op->ready, hipEventDisableTiming));
-                HIP_CHECK(ctx, hipEventRecord(op->ready, ctx->comm));
                 ring.sends[{ctx->rank, ops[k].peer}].push_back(op);
                 loop_match(ring, ctx->rank, ops[k].peer);
             } else {
                 ring.recvs[{ops[k].peer, ctx->rank}].push_back(op);
                 loop_match(ring, ops[k].peer, ctx->rank);
             }
-            mine.push_back(op);
         }
         ring.cv.notify_all();
         const bool ok = ring.cv.wait_for(lk, std::chrono::seconds(120), [&] {
