@@ -52,6 +52,9 @@ constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
 #endif
 constexpr int kHgPF = GOL_HG_PF;     // multistep_hg_kernel: rows prefetched ahead (< kMRing)
 static_assert(kHgPF >= 1 && kHgPF < kMRing, "prefetch slots");
+#ifndef GOL_IDLE_LANES_OFF
+#define GOL_IDLE_LANES_OFF 1        // multistep_hg_kernel: lanes past the last strip's halo lane exit
+#endif
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
 
@@ -865,6 +868,18 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         const int nout = min(kOut, p.wwords - s0);
         const int col = s0 + (lane - 1) * VEC;
         const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
+#if GOL_IDLE_LANES_OFF
+        // The last strip of a row owns fewer than 62 lanes' words (4 of 62 pairs
+        // at 262144 columns, 32 at 65536): lanes past its right halo lane would
+        // only compute garbage.  Switch them off -- an exec-masked lane issues
+        // nothing of its own and toggles no register bits, and this kernel is
+        // held at its power limit (DESIGN.md §4 "Clock").  DPP reads a
+        // switched-off lane as zero (bound_ctrl), as it reads past lane 63.
+        // The hashed instances keep every lane: hash_flush reduces across all 64.
+        if constexpr (!HASH) {
+            if (lane > (nout + VEC - 1) / VEC + 1) return;
+        }
+#endif
         int lcol;
         bool incol;
         if (p.wrap_x) {
