@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
@@ -35,6 +36,36 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
                 b[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0x96);
                 c[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)b[i], 0x130, 0xf, 0xf, true) ^ a[i];
                 a[i] = __builtin_amdgcn_bitop3_b32(a[i], b[i], c[i], 0xe8);
+            } else if constexpr (MODE == 4) {
+                // round-3 loop mix per 32-bit word (multistep_hg_kernel on the pair layout):
+                // a pair (e = a, o = b) arrives -- 2 DPP wave shifts, 2 v_alignbit, 4 v_bitop3 --
+                // and each of its words goes through the 7-v_bitop3 full-sum rule with the two
+                // previous rows' sums (kept in c and in the chain's state): 22 ops per pair
+                const uint32_t e = a[i], o = b[i];
+                const uint32_t left = (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x138, 0xf, 0xf, true);
+                const uint32_t right = (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x130, 0xf, 0xf, true);
+                const uint32_t we = __builtin_amdgcn_alignbit(o, left, 31);
+                const uint32_t eo = __builtin_amdgcn_alignbit(right, e, 1);
+                const uint32_t h0e = __builtin_amdgcn_bitop3_b32(we, e, o, 0x96);
+                const uint32_t h1e = __builtin_amdgcn_bitop3_b32(we, e, o, 0xe8);
+                const uint32_t h0o = __builtin_amdgcn_bitop3_b32(e, o, eo, 0x96);
+                const uint32_t h1o = __builtin_amdgcn_bitop3_b32(e, o, eo, 0xe8);
+                uint32_t out2[2];
+                const uint32_t hh0[2] = {h0e, h0o}, hh1[2] = {h1e, h1o};
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {  // rows A = c (plane 0) / c ^ 1 (plane 1), C = previous, B = new
+                    const uint32_t a0 = c[i], a1 = c[i] ^ 0x5a5a5a5au, c0 = hh0[j ^ 1], c1 = hh1[j ^ 1];
+                    const uint32_t e1 = __builtin_amdgcn_bitop3_b32(a0, c0, hh0[j], 0x69);
+                    const uint32_t e2 = __builtin_amdgcn_bitop3_b32(a0, c0, hh0[j], 0x7e);
+                    const uint32_t f1 = __builtin_amdgcn_bitop3_b32(a1, c1, hh1[j], 0x69);
+                    const uint32_t f2 = __builtin_amdgcn_bitop3_b32(a1, c1, hh1[j], 0x7e);
+                    const uint32_t t1 = __builtin_amdgcn_bitop3_b32(e1, e2, f2, 0x56);
+                    const uint32_t t2 = __builtin_amdgcn_bitop3_b32(e1, j ? o : e, t1, 0x45);
+                    out2[j] = __builtin_amdgcn_bitop3_b32(e2, f1, t2, 0x28);
+                }
+                c[i] = h0e;
+                a[i] = out2[0];
+                b[i] = out2[1];
             } else {  // step-kernel mix: 1 DPP, 2 alignbit, 9 bitop3, 1 xor  (13)
                 const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[i], 0x138, 0xf, 0xf, true);
                 const uint32_t w = __builtin_amdgcn_alignbit(a[i], l, 31);
@@ -88,7 +119,15 @@ int main() {
     int cus = 0; hipDeviceProp_t prop; CHK(hipGetDeviceProperties(&prop, 0)); cus = prop.multiProcessorCount;
     uint32_t* out; unsigned long long* clk;
     CHK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4)); CHK(hipMalloc(&clk, 16));
-    for (int w : {1, 2, 4, 5, 8}) {
+    const bool r3 = getenv("VALU_RATE_R3") != nullptr;  // only the round-3 loop mix, at 1..8 waves/SIMD
+    for (int w : {1, 2, 3, 4, 5, 6, 8}) {
+        if (r3) {
+            run<4, 2>("hg loop mix (22 ops/pair)", 22, w, out, clk, cus);
+            run<4, 4>("hg loop mix (22 ops/pair)", 22, w, out, clk, cus);
+            run<0, 4>("bitop3 x4", 4, w, out, clk, cus);
+            continue;
+        }
+        if (w == 3 || w == 6) continue;
         run<0, 4>("bitop3 x4", 4, w, out, clk, cus);
         run<1, 4>("alignbit x4", 4, w, out, clk, cus);
         run<2, 4>("dpp+xor/bitop3", 4, w, out, clk, cus);
