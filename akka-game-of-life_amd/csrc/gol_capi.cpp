@@ -592,8 +592,25 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
 // snapshot or a hash sees the whole plane.  A missing neighbour (clipped
 // board ends) reads dead rows: zero_row holds kMaxGensPerPass of them at the
 // halo pitch.
-int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
-                         const hipEvent_t* halo_ready, int nready) {
+// The interior rows [G, rows - G) of a sharded pass on the compute stream:
+// they read no halo, so they are enqueued before the exchange (one_pass) and
+// run while it is in flight.  Shards of <= 2G rows have no interior.
+int sharded_interior(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down) {
+    const int32_t rows = (int32_t)ctx->rows;
+    if (rows <= 2 * G) return GOL_OK;
+    const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
+    const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
+    const int32_t lo[1] = {G}, hi[1] = {rows - G};
+    return launch_ranges(ctx, G, ctx->plane[ctx->cur], ctx->plane[ctx->cur ^ 1], htop, hbot, ctx->pitch, false, slots,
+                         1, lo, hi, true);
+}
+
+// The rest of a sharded pass once every event in `halo_ready` has fired: the
+// two boundary row blocks on the edge stream (concurrent with the tail of the
+// interior launch, taking the slots its waves free; the compute stream waits
+// for them before the next pass), or the whole shard when it has no interior.
+int sharded_boundary(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
+                     const hipEvent_t* halo_ready, int nready) {
     uint32_t* cur = ctx->plane[ctx->cur];
     uint32_t* nxt = ctx->plane[ctx->cur ^ 1];
     const int32_t rows = (int32_t)ctx->rows;
@@ -601,15 +618,12 @@ int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool ha
     const uint32_t* htop = has_up ? ctx->halo_top : ctx->zero_row;
     const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
     if (rows > 2 * G) {
-        const int32_t lo[1] = {G}, hi[1] = {rows - G};
-        int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
-        if (rc) return rc;
         // The exchange events follow this pass's ev_ready, recorded on the
         // compute stream after the previous pass's boundary rows: every
         // reader of the plane the boundary kernels overwrite has finished.
         for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->edge, halo_ready[k], 0));
         const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
-        rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false, ctx->edge);
+        int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false, ctx->edge);
         if (rc) return rc;
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_edge, ctx->edge));
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_edge, 0));
@@ -618,6 +632,15 @@ int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool ha
     for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
     const int32_t lo[1] = {0}, hi[1] = {rows};
     return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
+}
+
+// Kernels of one sharded pass whose halos are already on their way (the
+// in-process group): the interior rows, then the boundary rows after
+// `halo_ready`.
+int sharded_pass_kernels(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
+                         const hipEvent_t* halo_ready, int nready) {
+    if (int rc = sharded_interior(ctx, G, slots, has_up, has_down)) return rc;
+    return sharded_boundary(ctx, G, slots, has_up, has_down, halo_ready, nready);
 }
 
 // One point-to-point operation of a pass's halo exchange: send `count`
@@ -795,8 +818,13 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         const int down = (ctx->rank + 1) % ctx->nranks;
         const bool has_up = torus || ctx->rank > 0;
         const bool has_down = torus || ctx->rank < ctx->nranks - 1;
-        // G-deep halo exchange on the comm stream once the current plane is final.
+        // G-deep halo exchange on the comm stream once the current plane is
+        // final (ev_ready: recorded before this pass's interior launch, so the
+        // exchange does not wait for it).  The interior launch is enqueued
+        // first: the GPU starts it while the host is still inside the RCCL
+        // group calls.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
+        if (int rc = sharded_interior(ctx, G, slots, has_up, has_down)) return rc;
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
         const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
         // Issue order matters when up == down (2 ranks, or 1 rank sending to
@@ -825,7 +853,7 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         // The event covers the sends too: the next pass overwrites this plane
         // only after the boundary kernels, which wait for it.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
-        int rc = sharded_pass_kernels(ctx, G, slots, has_up, has_down, &ctx->ev_halo, 1);
+        int rc = sharded_boundary(ctx, G, slots, has_up, has_down, &ctx->ev_halo, 1);
         if (rc) return rc;
     }
     ctx->cur ^= 1;
