@@ -137,6 +137,28 @@ __device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VE
     }
 }
 
+// load_words with the non-temporal hint (NT) or without.
+#ifndef GOL_G1_BAND4
+#define GOL_G1_BAND4 1   // step_kernel: dedicated straight-line path for 4-row bands
+#endif
+#ifndef GOL_G1_NT_MID
+#define GOL_G1_NT_MID 1  // ... whose two middle rows (read by one wave only) load non-temporally
+#endif
+template <int VEC, bool NT>
+__device__ __forceinline__ void load_words_k(const uint32_t* rp, int col, Words<VEC>& d) {
+    if constexpr (NT && VEC == 4) {
+        const U32x4 v = __builtin_nontemporal_load(reinterpret_cast<const U32x4*>(rp + col));
+        d.w[0] = v[0]; d.w[1] = v[1]; d.w[2] = v[2]; d.w[3] = v[3];
+    } else if constexpr (NT && VEC == 2) {
+        const U32x2 v = __builtin_nontemporal_load(reinterpret_cast<const U32x2*>(rp + col));
+        d.w[0] = v[0]; d.w[1] = v[1];
+    } else if constexpr (NT) {
+        d.w[0] = __builtin_nontemporal_load(rp + col);
+    } else {
+        load_words<VEC>(rp, col, d);
+    }
+}
+
 // Store one lane's VEC words of an output row through a buffer descriptor
 // built from the (wave-uniform) row address: lanes that do not own their
 // words and rows outside the band get an out-of-range offset / a zero-sized
@@ -538,14 +560,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             load_words<VEC>(rp, lcolumn, d);
             e = rp[ecol];
         };
-        auto step_i = [&](int i, int u, bool in_band) {
-            const int ua = u % kRing, uc = (u + 1) % kRing, ub = (u + 2) % kRing;
+        // output row i from stream rows i (above), i + 1 (centre), i + 2 (below)
+        auto step_rows = [&](int i, const Words<VEC>& RA, const Words<VEC>& RC, const Words<VEC>& RB, uint32_t eA,
+                             uint32_t eC, uint32_t eB, bool in_band) {
             const bool va = row_visible<CLIPPED>(p, row_of(i));
             const bool vc = row_visible<CLIPPED>(p, row_of(i + 1));
             const bool vb = row_visible<CLIPPED>(p, row_of(i + 2));
             uint32_t v0[VEC], v1[VEC], p0[VEC], p1[VEC];
-            column_sums<VEC, CLIPPED>(ring[ua], ring[uc], ring[ub], va, vc, vb, cmask, v0, v1, p0, p1);
-            uint32_t eA = edge[ua], eC = edge[uc], eB = edge[ub];
+            column_sums<VEC, CLIPPED>(RA, RC, RB, va, vc, vb, cmask, v0, v1, p0, p1);
             if constexpr (CLIPPED) {
                 eA = va ? (eA & emask) : 0u;
                 eC = vc ? (eC & emask) : 0u;
@@ -567,7 +589,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 n1 = last ? r1 : n1;
             }
             Words<VEC> o;
-            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, ring[uc], o);
+            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, RC, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -578,20 +600,48 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 if (in_band) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc);
             }
         };
+        auto step_i = [&](int i, int u, bool in_band) {
+            const int ua = u % kRing, uc = (u + 1) % kRing, ub = (u + 2) % kRing;
+            step_rows(i, ring[ua], ring[uc], ring[ub], edge[ua], edge[uc], edge[ub], in_band);
+        };
 
-        // Loads are never predicated: stream rows past the band's last one
-        // are clamped to it, and steps past the band compute into the void
-        // (their stores are skipped), so the loop body is straight-line.
-        const int tmax = nrows + 1;
+#if GOL_G1_BAND4
+        if (nrows == 4) {
+            // The single-generation pass's own band height (pick_band): its six
+            // stream rows issued at once, each exactly once, and four steps.
+            // The two middle rows are read by this wave alone -- every other
+            // row is also a neighbouring band's halo or edge row and is kept
+            // in the caches for that second reader -- so they are loaded
+            // non-temporally (GOL_G1_NT_MID).
+            Words<VEC> r6[6];
+            uint32_t e6[6];
+            static_for<6>([&](auto T) __attribute__((always_inline)) {
+                constexpr int t = decltype(T)::value;
+                const uint32_t* rp = row_ptr(p, row_of(t), 1);
+                load_words_k<VEC, GOL_G1_NT_MID != 0 && (t == 2 || t == 3)>(rp, lcolumn, r6[t]);
+                e6[t] = rp[ecol];
+            });
+            static_for<4>([&](auto I) __attribute__((always_inline)) {
+                constexpr int i = decltype(I)::value;
+                step_rows(i, r6[i], r6[i + 1], r6[i + 2], e6[i], e6[i + 1], e6[i + 2], true);
+            });
+        } else
+#endif
+        {
+            // Loads are never predicated: stream rows past the band's last one
+            // are clamped to it, and steps past the band compute into the void
+            // (their stores are skipped), so the loop body is straight-line.
+            const int tmax = nrows + 1;
 #pragma unroll
-        for (int t = 0; t < kRing - 1; ++t) load_t(min(t, tmax), ring[t], edge[t]);
-        for (int i0 = 0; i0 < nrows; i0 += kRing) {
+            for (int t = 0; t < kRing - 1; ++t) load_t(min(t, tmax), ring[t], edge[t]);
+            for (int i0 = 0; i0 < nrows; i0 += kRing) {
 #pragma unroll
-            for (int u = 0; u < kRing; ++u) {
-                const int i = i0 + u;
-                const int sl = (u + kRing - 1) % kRing;
-                load_t(min(i + kRing - 1, tmax), ring[sl], edge[sl]);
-                step_i(i, u, i < nrows);
+                for (int u = 0; u < kRing; ++u) {
+                    const int i = i0 + u;
+                    const int sl = (u + kRing - 1) % kRing;
+                    load_t(min(i + kRing - 1, tmax), ring[sl], edge[sl]);
+                    step_i(i, u, i < nrows);
+                }
             }
         }
         if constexpr (HASH) acc = hash_lane_total(hacc, col, active);
