@@ -361,11 +361,14 @@ int lane_words(const gol_ctx* ctx, int gens) {
 // `resident`: waves the whole GPU holds at once for this kernel (0: unknown).
 int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t resident) {
     if (ctx->band_rows > 0) return ctx->band_rows;
-    // Single-generation passes: 4-row bands -- more, shorter streams in
-    // flight; the band seams (2 halo rows per 4) hit the Infinity Cache.
-    // Same-box sweep (profiles/r02_g1_band_sweep.txt, ms per generation):
-    // 65536^2 0.197 (4) vs 0.209 (16), 262144^2 3.12 vs 3.45, x 32768 0.395 vs 0.420.
-    if (gens == 1) return 4;
+    // Single-generation passes: 6-row bands -- short streams, many in
+    // flight, each band's 8 rows issued at once by step_kernel's straight-line
+    // band path; the band seams (2 halo rows per 6) hit the caches.  Same-box
+    // sweep with the band paths (profiles/r03_g1_band_heights.txt, HBM
+    // fraction by kernel time, bands 4 / 6 / 8): 262144^2 0.738 / 0.774 /
+    // 0.755, x 32768 0.734 / 0.762 / 0.749, 65536^2 0.752 / 0.760 / 0.753
+    // (round 2, ring loop only: 4 rows best, profiles/r02_g1_band_sweep.txt).
+    if (gens == 1) return 6;
     // Multi-generation passes recompute 2G halo rows per band: keep bands
     // >= 64 rows, aim at ~8192 waves, cap at 256 rows.
     const int64_t bands = std::max<int64_t>(1, 8192 / std::max(1, strips));

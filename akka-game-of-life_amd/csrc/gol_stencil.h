@@ -606,25 +606,33 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
         };
 
 #if GOL_G1_BAND4
-        if (nrows == 4) {
-            // The single-generation pass's own band height (pick_band): its six
-            // stream rows issued at once, each exactly once, and four steps.
-            // The two middle rows are read by this wave alone -- every other
-            // row is also a neighbouring band's halo or edge row and is kept
-            // in the caches for that second reader -- so they are loaded
-            // non-temporally (GOL_G1_NT_MID).
-            Words<VEC> r6[6];
-            uint32_t e6[6];
-            static_for<6>([&](auto T) __attribute__((always_inline)) {
+        // The single-generation pass's own band heights (pick_band): the B + 2
+        // stream rows issued at once, each once, and B steps.  The B - 2
+        // middle rows are read by this wave alone -- the two edge rows and
+        // the two halo rows are also a neighbouring band's halo or edge rows,
+        // kept in the caches for that second reader -- so they load
+        // non-temporally (GOL_G1_NT_MID).
+        auto band_path = [&](auto BB) __attribute__((always_inline)) {
+            constexpr int B = decltype(BB)::value;
+            Words<VEC> rs[B + 2];
+            uint32_t es[B + 2];
+            static_for<B + 2>([&](auto T) __attribute__((always_inline)) {
                 constexpr int t = decltype(T)::value;
                 const uint32_t* rp = row_ptr(p, row_of(t), 1);
-                load_words_k<VEC, GOL_G1_NT_MID != 0 && (t == 2 || t == 3)>(rp, lcolumn, r6[t]);
-                e6[t] = rp[ecol];
+                load_words_k<VEC, GOL_G1_NT_MID != 0 && t >= 2 && t <= B - 1>(rp, lcolumn, rs[t]);
+                es[t] = rp[ecol];
             });
-            static_for<4>([&](auto I) __attribute__((always_inline)) {
+            static_for<B>([&](auto I) __attribute__((always_inline)) {
                 constexpr int i = decltype(I)::value;
-                step_rows(i, r6[i], r6[i + 1], r6[i + 2], e6[i], e6[i + 1], e6[i + 2], true);
+                step_rows(i, rs[i], rs[i + 1], rs[i + 2], es[i], es[i + 1], es[i + 2], true);
             });
+        };
+        if (nrows == 4) {
+            band_path(std::integral_constant<int, 4>{});
+        } else if (nrows == 6) {
+            band_path(std::integral_constant<int, 6>{});
+        } else if (nrows == 8) {
+            band_path(std::integral_constant<int, 8>{});
         } else
 #endif
         {

@@ -158,7 +158,7 @@ def test_unhashed_single_generation_torus(gpu, W, H, vec):
     check_run_unhashed_g1(W, H, 5, seed=W + H + vec, vec=vec)
 
 
-@pytest.mark.parametrize("band", [1, 3, 4, 16, 0])
+@pytest.mark.parametrize("band", [1, 3, 4, 6, 8, 16, 0])  # 4 / 6 / 8: step_kernel's straight-line band paths
 def test_unhashed_single_generation_bands_rules_clipped(gpu, band):
     check_run_unhashed_g1(32 * 520, 37, 4, seed=band, band=band)
     check_run_unhashed_g1(32 * 12, 29, 4, rule=(0x0C8, 0x1A6), seed=band, band=band)
