@@ -318,13 +318,28 @@ int stencil_variant() {
 
 // Blocks per XCD chunk of the step kernels' block order (gol_stencil.h
 // xcd_block).  GOL_XCD_CHUNK overrides (A/B experiments; 1 = dispatch order).
-int xcd_chunk() {
+int xcd_chunk_env() {  // 0: not set
     static const int c = [] {
         const char* e = getenv("GOL_XCD_CHUNK");
-        const int v = e ? atoi(e) : kDefaultXcdChunk;
+        if (!e) return 0;
+        const int v = atoi(e);
         return v < 1 ? 1 : (v > 64 ? 64 : v);
     }();
     return c;
+}
+
+// Multi-generation passes: kDefaultXcdChunk.  Single-generation passes (the
+// 6-row band paths, whose seams are read by two bands at about the same time):
+// four bands' blocks per XCD, so three of every four band seams stay in one
+// XCD's L2.  Same-box sweep (profiles/r03_g1_xcd_chunk.txt, HBM fraction by
+// kernel time, chunk 8 / 16 / 32 / 64): 262144^2 (8 blocks per band) 0.76-0.78
+// / 0.79-0.80 / 0.80 / 0.75-0.77, 65536^2 (2 blocks per band) 0.75 / 0.75 /
+// 0.73-0.75 / 0.72.
+int xcd_chunk(int gens, int strips) {
+    if (int c = xcd_chunk_env()) return c;
+    if (gens != 1) return kDefaultXcdChunk;
+    const int blocks_per_band = (strips + gol::kWavesPerWG - 1) / gol::kWavesPerWG;
+    return std::min(64, std::max(kDefaultXcdChunk, 4 * blocks_per_band));
 }
 
 // Kernel formulation a pass at `vec` words per lane actually runs: 16-byte
@@ -565,7 +580,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.birth = ctx->birth;
     p.survive = ctx->survive;
     p.variant = kernel_variant(vec);
-    p.xcd_chunk = xcd_chunk();
+    p.xcd_chunk = xcd_chunk(gens, p.strips);
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
     p.clk = nullptr;
