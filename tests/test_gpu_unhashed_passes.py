@@ -115,3 +115,25 @@ def test_unhashed_group(gpu, n, gpp):
         s.close()
     ref, _ = O.run_packed(full, W, gens, O.TORUS, O.LIFE, want_hashes=False)
     assert (board == ref).all()
+
+
+@pytest.mark.parametrize("gpp", [2, 5, 8])
+@pytest.mark.parametrize("W", [7, 100, 32 * 62 + 5, 32 * 130 - 9, 32 * 300 + 17])
+@pytest.mark.parametrize("rule", [O.REF_EFFECTIVE, O.REF_LITERAL, O.LIFE])
+def test_unhashed_clipped(gpu, W, gpp, rule):
+    """The reference geometry (ref-clipped, row-major words, any width) without
+    the fused hash: the unhashed clipped instances switch off the lanes past
+    their last strip's halo lane too (GOL_IDLE_LANES_OFF)."""
+    H = 23
+    rng = np.random.default_rng(W * 3 + gpp)
+    cells = (rng.random((H, W)) < 0.5).astype(np.uint8)
+    board = O.pack(cells)
+    with engine(W, H, topology="ref-clipped", rule=rule_obj(rule)) as e:
+        e.set_tuning(gens_per_pass=gpp)
+        e.load(board)
+        e.step(2 * gpp + 1)
+        h = e.hash()
+        final_gpu = e.snapshot()
+    final_cpu, want = O.run_packed(board, W, 2 * gpp + 1, O.REF_CLIPPED, rule)
+    np.testing.assert_array_equal(final_gpu, final_cpu)
+    assert h == int(want[-1])
