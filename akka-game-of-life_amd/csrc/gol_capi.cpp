@@ -10,6 +10,7 @@
 //                    NextStateCellGathererActor.scala:25-48)
 //   gol_snapshot <- CellStateMsg -> LoggerActor (CellActor.scala:89, LoggerActor.scala:30-46)
 //   gol_comm_*   <- cross-backend GetStateFromEpoch/StateForEpoch over Akka remote
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -35,9 +36,13 @@ namespace {
 std::mutex g_err_mu;
 std::string g_err;  // process-wide last error (gol_create failures)
 
+// What a profiled event pair brackets (gol_profile_stats).
+enum ProfKind { kProfNone = -1, kProfMain = 0, kProfExchange = 1, kProfBoundary = 2 };
+
 struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
     int clk_slot = -1;  // this launch's clock-probe slot (gol_stencil.h clock_probe_*), or -1
+    int kind = kProfMain;
 };
 
 // Clock-probe slots per context (one per profiled launch between folds).
@@ -109,6 +114,9 @@ struct gol_ctx {
     unsigned long long* clk_buf = nullptr;  // kClockSlots x kClockSlotWords u64 (device)
     uint32_t clk_used = 0;                  // slots handed out since the last fold
     double prof_clk_ms_ghz = 0.0, prof_clk_ms = 0.0;  // time-weighted probe clock
+    double prof_xchg_ms = 0.0, prof_bnd_ms = 0.0;     // halo exchanges (comm stream), boundary launches (edge)
+    uint64_t prof_xchg = 0, prof_bnd = 0;
+    uint64_t halo_sent = 0, halo_recv = 0;             // bytes posted to the ring since the last reset
     // occupancy
     int num_cus = 0;
     std::map<int, int64_t> occupancy_cache;
@@ -165,7 +173,12 @@ uint64_t g_absorbed = 0;
 std::string g_absorbed_last;
 std::map<std::string, int> g_absorb_seen;
 
-void absorb_rccl_status(const char* call) {
+// `pending_before`: the thread's status before the RCCL call
+// (hipPeekAtLastError).  If the caller had left one pending, whatever is
+// pending now may be the caller's own: it is left in place, not taken, counted
+// or attributed to RCCL.
+void absorb_rccl_status(const char* call, hipError_t pending_before) {
+    if (pending_before != hipSuccess) return;
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) return;
     char msg[256];
@@ -178,8 +191,9 @@ void absorb_rccl_status(const char* call) {
 
 #define NCCL_CHECK(ctx, expr)                                                                       \
     do {                                                                                            \
+        const hipError_t pre_ = hipPeekAtLastError();                                               \
         ncclResult_t r_ = (expr);                                                                   \
-        absorb_rccl_status(#expr);                                                                  \
+        absorb_rccl_status(#expr, pre_);                                                            \
         if (r_ != ncclSuccess)                                                                      \
             return set_err((ctx), GOL_ECOMM, "%s failed: %s (%s:%d)", #expr, ncclGetErrorString(r_), \
                            __FILE__, __LINE__);                                                     \
@@ -197,6 +211,17 @@ bool sharded(const gol_ctx* c) {
 }
 
 bool in_ring(const gol_ctx* c) { return c->nccl != nullptr || c->loop != nullptr; }
+
+// The B3/S23 torus: the only boards the fast-path kernel instances serve.
+bool life_torus(const gol_ctx* c) {
+    return c->topology == GOL_TORUS && c->birth == GOL_RULE_LIFE_BIRTH && c->survive == GOL_RULE_LIFE_SURVIVE;
+}
+
+// Deepest pass of the 16-byte-lane generic-rule and clipped kernel instances
+// that keeps every variable in registers: deeper ones spill (448-640 B of
+// scratch per lane from G = 8, hashed clipped, on; every one of them at
+// G >= 10; `make asm` resource usage).
+constexpr int kMaxGensVec4Generic = 7;
 
 int bind(gol_ctx* ctx) {
     HIP_CHECK(ctx, hipSetDevice(ctx->device));
@@ -258,6 +283,16 @@ int fold_profile(gol_ctx* ctx) {
     }
     for (size_t i = 0; i < ctx->evs_used; ++i) {
         const float ms = times[i];
+        if (ctx->evs[i].kind == kProfExchange) {
+            ctx->prof_xchg_ms += ms;
+            ctx->prof_xchg += 1;
+            continue;
+        }
+        if (ctx->evs[i].kind == kProfBoundary) {
+            ctx->prof_bnd_ms += ms;
+            ctx->prof_bnd += 1;
+            continue;
+        }
         ctx->prof_ms += ms;
         ctx->prof_launches += 1;
         const int slot = ctx->evs[i].clk_slot;
@@ -296,7 +331,10 @@ EventPair* next_event_pair(gol_ctx* ctx) {
             ctx->evs.push_back(e);
         }
     }
-    return &ctx->evs[ctx->evs_used++];
+    EventPair* ev = &ctx->evs[ctx->evs_used++];
+    ev->kind = kProfMain;
+    ev->clk_slot = -1;
+    return ev;
 }
 
 // Automatic tuning (scripts/tune.py sweeps on MI355X, profiles/r01_*):
@@ -524,7 +562,7 @@ struct PlaneGeom {
 // is the dominant kernel.
 int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, const uint32_t* htop,
                   const uint32_t* hbot, int64_t halo_stride, bool wrap_y, unsigned long long* slots, int n,
-                  const int32_t* lo, const int32_t* hi, bool main_launch, hipStream_t stream = nullptr,
+                  const int32_t* lo, const int32_t* hi, int prof_kind, hipStream_t stream = nullptr,
                   const PlaneGeom* geom = nullptr) {
     if (!stream) stream = ctx->compute;
     gol::StepParams p{};
@@ -584,35 +622,29 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
     p.clk = nullptr;
-    if (ctx->prof && main_launch) {
+    if (ctx->prof && prof_kind != kProfNone) {
         ev = next_event_pair(ctx);
         if (!ev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
-        if (ctx->clk_buf && ctx->clk_used < kClockSlots) {
+        ev->kind = prof_kind;
+        if (prof_kind == kProfMain && ctx->clk_buf && ctx->clk_used < kClockSlots) {
             ev->clk_slot = (int)ctx->clk_used++;
             p.clk = ctx->clk_buf + (size_t)ev->clk_slot * gol::kClockSlotWords;
         }
-        HIP_CHECK(ctx, hipEventRecord(ev->start, ctx->compute));
+        HIP_CHECK(ctx, hipEventRecord(ev->start, stream));
     }
     HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, 1, stream));
     if (ev) {
-        HIP_CHECK(ctx, hipEventRecord(ev->stop, ctx->compute));
-        ctx->prof_gens += (uint64_t)gens;
+        HIP_CHECK(ctx, hipEventRecord(ev->stop, stream));
+        if (prof_kind == kProfMain) ctx->prof_gens += (uint64_t)gens;
     }
     return GOL_OK;
 }
 
-// Kernels of one sharded pass: the interior rows [G, rows-G) -- they need no
-// halo and overlap the exchange -- on the compute stream, and the two
-// boundary row blocks on the edge stream once every event in `halo_ready`
-// has fired.  The boundary launch runs concurrently with the tail of the
-// interior one (its waves take the slots the interior's waves free) instead
-// of after it; the compute stream then waits for it, so the next pass, a
-// snapshot or a hash sees the whole plane.  A missing neighbour (clipped
-// board ends) reads dead rows: zero_row holds kMaxGensPerPass of them at the
-// halo pitch.
 // The interior rows [G, rows - G) of a sharded pass on the compute stream:
 // they read no halo, so they are enqueued before the exchange (one_pass) and
-// run while it is in flight.  Shards of <= 2G rows have no interior.
+// run while it is in flight.  Shards of <= 2G rows have no interior.  A
+// missing neighbour (clipped board ends) reads dead rows: zero_row holds
+// kMaxGensPerPass of them at the halo pitch.
 int sharded_interior(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down) {
     const int32_t rows = (int32_t)ctx->rows;
     if (rows <= 2 * G) return GOL_OK;
@@ -620,13 +652,15 @@ int sharded_interior(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up
     const uint32_t* hbot = has_down ? ctx->halo_bot : ctx->zero_row;
     const int32_t lo[1] = {G}, hi[1] = {rows - G};
     return launch_ranges(ctx, G, ctx->plane[ctx->cur], ctx->plane[ctx->cur ^ 1], htop, hbot, ctx->pitch, false, slots,
-                         1, lo, hi, true);
+                         1, lo, hi, kProfMain);
 }
 
 // The rest of a sharded pass once every event in `halo_ready` has fired: the
-// two boundary row blocks on the edge stream (concurrent with the tail of the
-// interior launch, taking the slots its waves free; the compute stream waits
-// for them before the next pass), or the whole shard when it has no interior.
+// two boundary row blocks on the edge stream, or the whole shard when it has
+// no interior.  The boundary launch runs concurrently with the tail of the
+// interior one (its waves take the slots the interior's waves free) instead
+// of after it; the compute stream then waits for it, so the next pass, a
+// snapshot or a hash sees the whole plane.
 int sharded_boundary(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up, bool has_down,
                      const hipEvent_t* halo_ready, int nready) {
     uint32_t* cur = ctx->plane[ctx->cur];
@@ -641,7 +675,8 @@ int sharded_boundary(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up
         // reader of the plane the boundary kernels overwrite has finished.
         for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->edge, halo_ready[k], 0));
         const int32_t blo[2] = {0, rows - G}, bhi[2] = {G, rows};
-        int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, false, ctx->edge);
+        int rc = launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 2, blo, bhi, kProfBoundary,
+                               ctx->edge);
         if (rc) return rc;
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_edge, ctx->edge));
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, ctx->ev_edge, 0));
@@ -649,7 +684,7 @@ int sharded_boundary(gol_ctx* ctx, int G, unsigned long long* slots, bool has_up
     }
     for (int k = 0; k < nready; ++k) HIP_CHECK(ctx, hipStreamWaitEvent(ctx->compute, halo_ready[k], 0));
     const int32_t lo[1] = {0}, hi[1] = {rows};
-    return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, true);
+    return launch_ranges(ctx, G, cur, nxt, htop, hbot, pitch, false, slots, 1, lo, hi, kProfMain);
 }
 
 // Kernels of one sharded pass whose halos are already on their way (the
@@ -681,11 +716,18 @@ struct HaloOp {
 // sender's plane was final (an event on the sender's comm stream) and before
 // the sender's stream goes on (an event the sender's comm stream waits for),
 // as an RCCL send / recv pair is.  Test transport: the product path is RCCL.
+// A ring fails when a rank times out waiting for a peer, leaves it, or
+// mismatches an all-reduce: every waiting and later operation of the other
+// ranks then returns GOL_ECOMM at once instead of waiting out its timeout,
+// and its key cannot be joined again while members still hold it.
 struct LoopRing {
     std::mutex mu;
     std::condition_variable cv;
     int nranks = 0;
     int joined = 0;
+    std::vector<bool> present;  // ranks currently joined
+    bool failed = false;
+    std::string why;            // first failure
     struct Op {
         gol_ctx* ctx;
         uint32_t* buf;
@@ -738,9 +780,46 @@ void loop_match(LoopRing& ring, int src, int dst) {
     }
 }
 
+// How long a loopback rank waits for its peers (GOL_LOOPBACK_TIMEOUT_MS,
+// default 120 s; tests shorten it).
+std::chrono::milliseconds loop_timeout() {
+    const char* e = getenv("GOL_LOOPBACK_TIMEOUT_MS");
+    const long v = e ? atol(e) : 0;
+    return std::chrono::milliseconds(v > 0 ? v : 120000);
+}
+
+// Mark the ring failed (ring lock held) and wake every waiting rank.
+void loop_fail(LoopRing& ring, const std::string& why) {
+    if (!ring.failed) {
+        ring.failed = true;
+        ring.why = why;
+    }
+    ring.cv.notify_all();
+}
+
+// Take this context's unmatched operations out of the ring's queues (ring
+// lock held), so no peer can match them after the context stops waiting:
+// they hold its plane pointers and events, which may be gone by then.
+void loop_purge(LoopRing& ring, const gol_ctx* ctx) {
+    for (auto* qs : {&ring.sends, &ring.recvs})
+        for (auto& kv : *qs) {
+            auto& q = kv.second;
+            q.erase(std::remove_if(q.begin(), q.end(),
+                                   [&](const std::shared_ptr<LoopRing::Op>& o) { return o->ctx == ctx && !o->matched; }),
+                    q.end());
+        }
+}
+
 int loop_exchange(gol_ctx* ctx, const HaloOp* ops, int n) {
     LoopRing& ring = *ctx->loop;
     std::vector<std::shared_ptr<LoopRing::Op>> mine;
+    auto destroy_events = [&]() {
+        for (auto& o : mine)
+            if (o->ready) {
+                hip_note(hipEventDestroy(o->ready), "loopback: hipEventDestroy");
+                o->ready = nullptr;
+            }
+    };
     // Every send's event is created and recorded before any operation is
     // posted, so a failure here leaves nothing in the ring for a peer to match.
     for (int k = 0; k < n; ++k) {
@@ -753,13 +832,17 @@ int loop_exchange(gol_ctx* ctx, const HaloOp* ops, int n) {
         hipError_t e = hipEventCreateWithFlags(&op->ready, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventRecord(op->ready, ctx->comm);
         if (e != hipSuccess) {
-            for (auto& o : mine)
-                if (o->ready) hip_note(hipEventDestroy(o->ready), "loopback: hipEventDestroy");
+            destroy_events();
             return hip_fail(ctx, e, "loopback: send event", __FILE__, __LINE__);
         }
     }
     {
         std::unique_lock<std::mutex> lk(ring.mu);
+        if (ring.failed) {
+            lk.unlock();
+            destroy_events();
+            return set_err(ctx, GOL_ECOMM, "loopback ring failed: %s", ring.why.c_str());
+        }
         for (int k = 0; k < n; ++k) {
             auto& op = mine[k];
             if (ops[k].send) {
@@ -771,48 +854,87 @@ int loop_exchange(gol_ctx* ctx, const HaloOp* ops, int n) {
             }
         }
         ring.cv.notify_all();
-        const bool ok = ring.cv.wait_for(lk, std::chrono::seconds(120), [&] {
-            return std::all_of(mine.begin(), mine.end(), [](const auto& o) { return o->matched; });
-        });
-        if (!ok) return set_err(ctx, GOL_ECOMM, "loopback ring: a peer never posted its halo operations");
+        auto all_matched = [&] { return std::all_of(mine.begin(), mine.end(), [](const auto& o) { return o->matched; }); };
+        ring.cv.wait_for(lk, loop_timeout(), [&] { return all_matched() || ring.failed; });
+        if (!all_matched()) {
+            // timed out, or the ring failed under us: nothing of ours may be
+            // matched later
+            loop_purge(ring, ctx);
+            if (!ring.failed)
+                loop_fail(ring, "rank " + std::to_string(ctx->rank) + " timed out waiting for a peer's halo operations");
+            std::string why = ring.why;
+            lk.unlock();
+            bind(ctx);
+            destroy_events();
+            return set_err(ctx, GOL_ECOMM, "loopback ring: %s", why.c_str());
+        }
     }
     int rc = bind(ctx);  // a match made on this thread may have switched devices
-    for (auto& op : mine) {
-        if (op->ready) hip_note(hipEventDestroy(op->ready), "loopback: hipEventDestroy");
+    for (auto& op : mine)
         if (op->err && !rc) rc = set_err(ctx, op->err, "loopback ring: halo operation failed");
-    }
+    destroy_events();
     return rc;
 }
 
 int loop_allreduce(gol_ctx* ctx, uint64_t* values, uint32_t count) {
     LoopRing& ring = *ctx->loop;
     std::unique_lock<std::mutex> lk(ring.mu);
-    if (ring.arrived == 0) ring.acc.assign(values, values + count);
-    else if (ring.acc.size() != count) return set_err(ctx, GOL_EINVAL, "loopback all-reduce: counts differ");
-    else for (uint32_t k = 0; k < count; ++k) ring.acc[k] += values[k];
+    if (ring.failed) return set_err(ctx, GOL_ECOMM, "loopback ring failed: %s", ring.why.c_str());
+    if (ring.arrived == 0) {
+        ring.acc.assign(values, values + count);
+    } else if (ring.acc.size() != count) {
+        loop_fail(ring, "all-reduce counts differ between ranks");
+        return set_err(ctx, GOL_EINVAL, "loopback all-reduce: counts differ");
+    } else {
+        for (uint32_t k = 0; k < count; ++k) ring.acc[k] += values[k];
+    }
     const uint64_t my_round = ring.round;
     if (++ring.arrived == ring.nranks) {
         ring.result = ring.acc;
         ring.arrived = 0;
         ++ring.round;
         ring.cv.notify_all();
-    } else if (!ring.cv.wait_for(lk, std::chrono::seconds(120), [&] { return ring.round != my_round; })) {
-        return set_err(ctx, GOL_ECOMM, "loopback all-reduce: a peer never joined");
+    } else {
+        ring.cv.wait_for(lk, loop_timeout(), [&] { return ring.round != my_round || ring.failed; });
+        if (ring.round == my_round) {
+            if (!ring.failed) loop_fail(ring, "rank " + std::to_string(ctx->rank) + " timed out in an all-reduce");
+            return set_err(ctx, GOL_ECOMM, "loopback all-reduce: %s", ring.why.c_str());
+        }
     }
     std::copy(ring.result.begin(), ring.result.end(), values);
     return GOL_OK;
 }
 
+// Leave the ring: this context's unmatched operations are withdrawn, and a
+// ring left while others are still in it is failed, so they do not wait for
+// a rank that is gone.
 void loop_leave(gol_ctx* ctx) {
     if (!ctx->loop) return;
     std::lock_guard<std::mutex> lk(g_loop_mu);
     {
-        std::lock_guard<std::mutex> rl(ctx->loop->mu);
-        --ctx->loop->joined;
+        LoopRing& ring = *ctx->loop;
+        std::lock_guard<std::mutex> rl(ring.mu);
+        loop_purge(ring, ctx);
+        --ring.joined;
+        if (ctx->rank >= 0 && (size_t)ctx->rank < ring.present.size()) ring.present[ctx->rank] = false;
+        if (ring.joined > 0) loop_fail(ring, "rank " + std::to_string(ctx->rank) + " left the ring");
     }
     ctx->loop.reset();
     for (auto it = g_loops.begin(); it != g_loops.end();)
         it = it->second.expired() ? g_loops.erase(it) : std::next(it);
+}
+
+// A pass's halo operations as one RCCL group on the comm stream.
+int rccl_exchange(gol_ctx* ctx, const HaloOp* ops, int nops) {
+    NCCL_CHECK(ctx, ncclGroupStart());
+    for (int k = 0; k < nops; ++k) {
+        if (ops[k].send)
+            NCCL_CHECK(ctx, ncclSend(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
+        else
+            NCCL_CHECK(ctx, ncclRecv(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
+    }
+    NCCL_CHECK(ctx, ncclGroupEnd());
+    return GOL_OK;
 }
 
 // One pass of G generations (temporal blocking, G <= kMaxGensPerPass) of a
@@ -827,7 +949,7 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
     if (!sharded(ctx)) {
         // torus: rows wrap inside the plane; clipped: outside rows are dead
         const int32_t lo[1] = {0}, hi[1] = {rows};
-        int rc = launch_ranges(ctx, G, cur, nxt, ctx->zero_row, ctx->zero_row, 0, torus, slots, 1, lo, hi, true);
+        int rc = launch_ranges(ctx, G, cur, nxt, ctx->zero_row, ctx->zero_row, 0, torus, slots, 1, lo, hi, kProfMain);
         if (rc) return rc;
     } else if (ctx->group) {
         return set_err(ctx, GOL_ESTATE, "context belongs to a shard group: step it with gol_group_step");
@@ -840,9 +962,12 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         // final (ev_ready: recorded before this pass's interior launch, so the
         // exchange does not wait for it).  The interior launch is enqueued
         // first: the GPU starts it while the host is still inside the RCCL
-        // group calls.
+        // group calls.  If it cannot be enqueued, the halo operations are
+        // still posted before the error is returned: the peers' groups then
+        // complete instead of blocking in ncclGroupEnd until someone aborts
+        // the communicator.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
-        if (int rc = sharded_interior(ctx, G, slots, has_up, has_down)) return rc;
+        const int rc_interior = sharded_interior(ctx, G, slots, has_up, has_down);
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
         const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
         // Issue order matters when up == down (2 ranks, or 1 rank sending to
@@ -856,18 +981,25 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         if (has_up) ops[nops++] = {true, cur, cnt, up};
         if (has_up) ops[nops++] = {false, ctx->halo_top, cnt, up};
         if (has_down) ops[nops++] = {false, ctx->halo_bot, cnt, down};
-        if (ctx->loop) {
-            if (int rc = loop_exchange(ctx, ops, nops)) return rc;
-        } else {
-            NCCL_CHECK(ctx, ncclGroupStart());
-            for (int k = 0; k < nops; ++k) {
-                if (ops[k].send)
-                    NCCL_CHECK(ctx, ncclSend(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
-                else
-                    NCCL_CHECK(ctx, ncclRecv(ops[k].buf, ops[k].count, ncclUint32, ops[k].peer, ctx->nccl, ctx->comm));
-            }
-            NCCL_CHECK(ctx, ncclGroupEnd());
+        // exchange timing (gol_profile_stats): comm-stream events around the group
+        EventPair* xev = nullptr;
+        if (ctx->prof && rc_interior == GOL_OK) {
+            xev = next_event_pair(ctx);
+            if (!xev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
+            xev->kind = kProfExchange;
+            HIP_CHECK(ctx, hipEventRecord(xev->start, ctx->comm));
         }
+        for (int k = 0; k < nops; ++k) (ops[k].send ? ctx->halo_sent : ctx->halo_recv) += ops[k].count * 4;
+        const int rc_x = ctx->loop ? loop_exchange(ctx, ops, nops) : rccl_exchange(ctx, ops, nops);
+        if (xev) {
+            if (rc_x == GOL_OK) {
+                HIP_CHECK(ctx, hipEventRecord(xev->stop, ctx->comm));
+            } else {
+                --ctx->evs_used;  // the pair stays unrecorded: hand it back (it was the last one taken)
+            }
+        }
+        if (rc_interior) return rc_interior;
+        if (rc_x) return rc_x;
         // The event covers the sends too: the next pass overwrites this plane
         // only after the boundary kernels, which wait for it.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
@@ -959,11 +1091,12 @@ int group_pass(gol_group* g, int G, const std::vector<unsigned long long*>& slot
 constexpr int kMaxGensPlannedGeneric = 8;
 
 int depth_cap(const gol_ctx* ctx) {
-    const bool life_torus = ctx->topology == GOL_TORUS && ctx->birth == GOL_RULE_LIFE_BIRTH &&
-                            ctx->survive == GOL_RULE_LIFE_SURVIVE;
     int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass
-                                       : (life_torus ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
+                                       : (life_torus(ctx) ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
+    // 16-byte lanes forced by tuning: the generic-rule / clipped instances
+    // deeper than this spill (gol_set_tuning refuses them as fixed depths)
+    if (ctx->vec_fixed == 4 && !life_torus(ctx)) G = std::min<int64_t>(G, kMaxGensVec4Generic);
     if (in_ring(ctx)) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return (int)std::max<int64_t>(G, 1);
@@ -1045,8 +1178,9 @@ void destroy_impl(gol_ctx* c) {
         if (st) hip_note(hipStreamSynchronize(st), "destroy: hipStreamSynchronize");
     loop_leave(c);
     if (c->nccl) {
+        const hipError_t pre = hipPeekAtLastError();
         const ncclResult_t r = ncclCommDestroy(c->nccl);
-        absorb_rccl_status("ncclCommDestroy");
+        absorb_rccl_status("ncclCommDestroy", pre);
         if (r != ncclSuccess) fprintf(stderr, "libgol: destroy: ncclCommDestroy: %s\n", ncclGetErrorString(r));
         c->nccl = nullptr;
     }
@@ -1141,6 +1275,24 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     const int64_t wwords = (c.width + 31) / 32;
     if (wwords > (1 << 30) || rows > (1 << 30))
         return set_err(nullptr, GOL_EINVAL, "board too large");
+    if (c.topology == GOL_REF_CLIPPED) {
+        // The reference never completes a generation on a board where some
+        // cell has no visible neighbour: that cell's gatherer asks nobody, so
+        // no StateForEpoch ever arrives to complete it
+        // (NextStateCellGathererActor.scala:26-27,39-47); it retries, fails
+        // (:49-53) and re-asks for neighbours forever (CellActor.scala:92-94),
+        // never committing epoch 1, and every neighbour's request for that
+        // epoch stays queued (:75-76).  Such boards are refused rather than
+        // advanced with results the reference never produces.
+        const int64_t vw = c.vis_width > 0 ? c.vis_width : c.width - 1;
+        const int64_t vh = c.vis_height > 0 ? c.vis_height : c.height - 1;
+        if (vw < 1 || vh < 1 || (vw == 1 && vh == 1) || c.width > vw + 1 || c.height > vh + 1)
+            return set_err(nullptr, GOL_EINVAL,
+                           "ref-clipped board %lld x %lld with visible extents %lld x %lld: a cell has no visible "
+                           "neighbour, and the reference never completes a generation on such a board "
+                           "(NextStateCellGathererActor.scala:26-27,39-58, CellActor.scala:75-76,92-94)",
+                           (long long)c.width, (long long)c.height, (long long)vw, (long long)vh);
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
         (void)hipGetLastError();
@@ -1372,7 +1524,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     int cur = 0;
     for (int64_t g = 0; g < n; ++g) {
         if (int rc = launch_ranges(ctx, 1, blk[cur], blk[cur ^ 1], ctx->zero_row, ctx->zero_row, 0, false, nullptr, 1,
-                                   lo, hi, false, ctx->compute, &geom)) {
+                                   lo, hi, kProfNone, ctx->compute, &geom)) {
             release();
             return rc;
         }
@@ -1665,7 +1817,11 @@ int gol_comm_init_loopback(gol_ctx* ctx, const char* key, int rank, int nranks) 
     }
     std::lock_guard<std::mutex> rl(ring->mu);
     if (ring->nranks != nranks) return set_err(ctx, GOL_EINVAL, "loopback ring %s has %d ranks", key, ring->nranks);
+    if (ring->failed) return set_err(ctx, GOL_ESTATE, "loopback ring %s has failed (%s): join a new key", key, ring->why.c_str());
     if (ring->joined >= nranks) return set_err(ctx, GOL_ESTATE, "loopback ring %s is full", key);
+    if (ring->present.empty()) ring->present.assign(nranks, false);
+    if (ring->present[rank]) return set_err(ctx, GOL_EINVAL, "loopback ring %s: rank %d already joined", key, rank);
+    ring->present[rank] = true;
     ++ring->joined;
     ctx->loop = ring;
     ctx->rank = rank;
@@ -1732,6 +1888,50 @@ int gol_profile_reset(gol_ctx* ctx) {
     ctx->prof_launches = 0;
     ctx->prof_gens = 0;
     ctx->prof_clk_ms_ghz = ctx->prof_clk_ms = 0.0;
+    ctx->prof_xchg_ms = ctx->prof_bnd_ms = 0.0;
+    ctx->prof_xchg = ctx->prof_bnd = 0;
+    ctx->halo_sent = ctx->halo_recv = 0;
+    return GOL_OK;
+}
+
+int gol_profile_stats_read(gol_ctx* ctx, gol_profile_stats* out) {
+    if (!ctx || !out) return set_err(ctx, GOL_EINVAL, "null argument");
+    if (int rc = bind(ctx)) return rc;
+    if (int rc = fold_profile(ctx)) return rc;
+    *out = gol_profile_stats{};
+    out->kernel_ms = ctx->prof_ms;
+    out->launches = ctx->prof_launches;
+    out->generations = ctx->prof_gens;
+    out->exchange_ms = ctx->prof_xchg_ms;
+    out->exchanges = ctx->prof_xchg;
+    out->boundary_ms = ctx->prof_bnd_ms;
+    out->boundary_launches = ctx->prof_bnd;
+    out->halo_bytes_sent = ctx->halo_sent;
+    out->halo_bytes_received = ctx->halo_recv;
+    out->clock_ghz = ctx->prof_clk_ms > 0.0 ? ctx->prof_clk_ms_ghz / ctx->prof_clk_ms : 0.0;
+    return GOL_OK;
+}
+
+int gol_runtime_info_get(gol_runtime_info* out) {
+    if (!out) return set_err(nullptr, GOL_EINVAL, "null argument");
+    *out = gol_runtime_info{};
+    out->abi_version = GOL_ABI_VERSION;
+    int v = 0;
+    if (hipRuntimeGetVersion(&v) == hipSuccess) out->hip_runtime_version = v;
+    else (void)hipGetLastError();
+    v = 0;
+    if (hipDriverGetVersion(&v) == hipSuccess) out->hip_driver_version = v;
+    else (void)hipGetLastError();
+    v = 0;
+    if (ncclGetVersion(&v) == ncclSuccess) out->rccl_version = v;
+    // the files the dynamic linker bound these symbols to
+    auto path_of = [](const void* sym, char* dst, size_t cap) {
+        Dl_info info{};
+        if (dladdr(sym, &info) && info.dli_fname) snprintf(dst, cap, "%s", info.dli_fname);
+    };
+    path_of(reinterpret_cast<const void*>(&hipRuntimeGetVersion), out->hip_library, sizeof out->hip_library);
+    path_of(reinterpret_cast<const void*>(&ncclGetVersion), out->rccl_library, sizeof out->rccl_library);
+    path_of(reinterpret_cast<const void*>(&gol_runtime_info_get), out->gol_library, sizeof out->gol_library);
     return GOL_OK;
 }
 
@@ -1745,6 +1945,11 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     if (words_per_lane > 0 && ctx->wwords % words_per_lane != 0)
         return set_err(ctx, GOL_EINVAL, "words_per_lane %d does not divide the %d words of a row", words_per_lane,
                        ctx->wwords);
+    if (words_per_lane == 4 && !life_torus(ctx) && gens_per_pass > kMaxGensVec4Generic)
+        return set_err(ctx, GOL_EINVAL,
+                       "words_per_lane 4 with gens_per_pass %d > %d: the generic-rule / clipped kernel instance "
+                       "would spill registers to scratch",
+                       gens_per_pass, kMaxGensVec4Generic);
     ctx->band_rows = band_rows;
     ctx->gens_per_pass = gens_per_pass;
     ctx->vec_fixed = words_per_lane;

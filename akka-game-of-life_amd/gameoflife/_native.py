@@ -54,6 +54,33 @@ class GolConfig(ctypes.Structure):
     ]
 
 
+class GolProfileStats(ctypes.Structure):
+    _fields_ = [
+        ("kernel_ms", ctypes.c_double),
+        ("launches", ctypes.c_uint64),
+        ("generations", ctypes.c_uint64),
+        ("exchange_ms", ctypes.c_double),
+        ("exchanges", ctypes.c_uint64),
+        ("boundary_ms", ctypes.c_double),
+        ("boundary_launches", ctypes.c_uint64),
+        ("halo_bytes_sent", ctypes.c_uint64),
+        ("halo_bytes_received", ctypes.c_uint64),
+        ("clock_ghz", ctypes.c_double),
+    ]
+
+
+class GolRuntimeInfo(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("hip_runtime_version", ctypes.c_int32),
+        ("hip_driver_version", ctypes.c_int32),
+        ("rccl_version", ctypes.c_int32),
+        ("hip_library", ctypes.c_char * 512),
+        ("rccl_library", ctypes.c_char * 512),
+        ("gol_library", ctypes.c_char * 512),
+    ]
+
+
 _c = ctypes
 _vp = ctypes.c_void_p
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -110,6 +137,8 @@ _SIGNATURES = {
     "gol_group_destroy": (None, [_vp]),
     "gol_diag_take_hip_error": (_c.c_int, [ctypes.POINTER(_c.c_int)]),
     "gol_diag_absorbed": (_c.c_int, [_u64p, _c.c_char_p, _c.c_size_t]),
+    "gol_profile_stats_read": (_c.c_int, [_vp, ctypes.POINTER(GolProfileStats)]),
+    "gol_runtime_info_get": (_c.c_int, [ctypes.POINTER(GolRuntimeInfo)]),
 }
 
 
@@ -185,3 +214,23 @@ def absorbed() -> tuple[int, str]:
     buf = ctypes.create_string_buffer(256)
     check(lib.gol_diag_absorbed(ctypes.byref(n), buf, len(buf)))
     return n.value, buf.value.decode()
+
+
+def _version(v: int, major_div: int, minor_div: int) -> str:
+    return f"{v // major_div}.{v % major_div // minor_div}.{v % minor_div}" if v else "unknown"
+
+
+def runtime_info() -> dict:
+    """The HIP runtime and RCCL this process's libgol is bound to, and the
+    files they were loaded from (gol_runtime_info_get; host-only)."""
+    ri = GolRuntimeInfo()
+    check(lib.gol_runtime_info_get(ctypes.byref(ri)))
+    return {"hip_runtime_version": ri.hip_runtime_version,
+            "hip_runtime": _version(ri.hip_runtime_version, 10_000_000, 100_000),
+            "hip_driver_version": ri.hip_driver_version,
+            "rccl_version": ri.rccl_version,
+            "rccl": _version(ri.rccl_version, 10_000, 100),
+            "hip_library": ri.hip_library.decode(errors="replace"),
+            "rccl_library": ri.rccl_library.decode(errors="replace"),
+            "gol_library": ri.gol_library.decode(errors="replace"),
+            "torch_loaded": "torch" in __import__("sys").modules}

@@ -221,6 +221,14 @@ class GolEngine:
         self._chk(N.lib.gol_profile_clock(self._h, ctypes.byref(g)))
         return g.value
 
+    def profile_stats(self) -> dict:
+        """gol_profile_stats_read: the profiled passes since the reset split
+        into the dominant launch, the halo exchange on the comm stream and the
+        boundary launches, with the halo bytes posted to the ring."""
+        st = N.GolProfileStats()
+        self._chk(N.lib.gol_profile_stats_read(self._h, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in N.GolProfileStats._fields_}
+
     def occupancy(self, gens_per_pass: int) -> tuple[int, int]:
         """(resident waves per CU, strip width in words) of a G-generation pass."""
         w, s = ctypes.c_int32(0), ctypes.c_int32(0)

@@ -32,6 +32,7 @@ import os
 import numpy as np
 
 from .elastic import blob_rows, light_cone_from
+from ._native import GolError
 from .engine import GolEngine, ShardGroup, host_array
 from .shard import shard_rows_py
 
@@ -110,7 +111,12 @@ class ShardedSimulation:
         if self._pending_epoch is None:
             return
         if landed is None:
-            landed = self.shards[lost].snapshot_landed()
+            # On a truly lost device the query itself fails: a checkpoint
+            # whose landing cannot be confirmed never existed.
+            try:
+                landed = self.shards[lost].snapshot_landed()
+            except GolError:
+                landed = False
         if landed:
             self._finish_checkpoint()
             return

@@ -13,7 +13,19 @@ under "secondary".
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 value = W*H*K / max-over-ranks wall time of the K timed generations (GCUPS),
-with the board already resident in HBM.
+with the board already resident in HBM.  Before its W warm-up steps every
+timed board is seeded, stepped untimed for a short settle (the chip's clock
+recovers over ~20 launches after an idle gap such as the 16 GiB allocation,
+profiles/r02_warmup_curve.txt) and re-seeded, so the timed epochs are W + K
+from the seed and every window's hash is checked against a committed golden
+table (tests/golden/bench_*.json).
+
+No torch: the process is one rank of the launcher (RANK / WORLD_SIZE /
+LOCAL_RANK from the environment), the RCCL unique id travels through a file
+keyed by MASTER_ADDR:MASTER_PORT and the launcher's pid, and the barriers and
+the max over ranks are gol_comm_allreduce_u64 calls on the shard's own
+communicator -- so libgol runs on the same HIP runtime and RCCL (/opt/rocm's)
+as the pytest GPU suite and a JVM host; the line's "runtime" field names them.
 
 roofline: the dominant kernel (the whole-shard launch at
 N = 1, a shard's interior-rows launch at N > 1) is bound by VALU issue, not by
@@ -32,9 +44,11 @@ HBM -- temporal blocking fuses 6-8 generations per pass over the plane.  So:
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -75,53 +89,107 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(n):
-    import torch
-    import torch.distributed as dist
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != n:
-        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}")
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    return torch, dist, rank, world, local
+class Job:
+    """This process's place in the launch (one process per GPU).
+
+    Ranks come from the launcher's environment (torch.distributed.run sets
+    RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Rank 0's RCCL
+    unique id reaches the other ranks through a file named after
+    MASTER_ADDR:MASTER_PORT and the launcher's pid (every local rank is its
+    child; one node); after the first barrier over the new communicator
+    every rank has read it, and rank 0 removes it.  Barriers and the
+    max over ranks are gol_comm_allreduce_u64 calls on the shard's own RCCL
+    communicator: no torch, no second collective library."""
+
+    def __init__(self, n):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != n:
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
+        self.eng = None  # the engine whose communicator carries the collectives
+
+    def uid_path(self):
+        key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
+                        os.environ.get("TORCHELASTIC_RUN_ID", ""), str(os.getppid())])
+        return os.path.join(tempfile.gettempdir(), "gol_bench_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16])
+
+    def join(self, eng, N, timeout=300.0):
+        """Attach `eng` to the job's RCCL ring (rank 0 makes the id)."""
+        path = self.uid_path()
+        if self.rank == 0:
+            uid = N.unique_id()
+            tmp = f"{path}.{os.getpid()}.tmp"
+            with open(tmp, "wb") as f:
+                f.write(uid)
+            os.replace(tmp, path)
+        else:
+            t0 = time.monotonic()
+            while True:
+                try:
+                    with open(path, "rb") as f:
+                        uid = f.read()
+                    if len(uid) == N.GOL_UNIQUE_ID_BYTES:
+                        break
+                except OSError:
+                    pass
+                if time.monotonic() - t0 > timeout:
+                    raise SystemExit(f"rank {self.rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s")
+                time.sleep(0.01)
+        eng.comm_init(uid, self.rank, self.world)
+        self.eng = eng
+        self.barrier()  # every rank has read the id
+        if self.rank == 0:
+            try:
+                os.unlink(path)
+            except OSError:
+                pass
+
+    def barrier(self):
+        if self.world > 1:
+            self.eng.allreduce_u64([0])
+
+    def gather(self, row):
+        """Every rank's `row` (equal-length u64 list): a world x len(row)
+        table, rank r in row r (an all-reduce of one-hot rows)."""
+        import numpy as np
+        k = len(row)
+        if self.world == 1:
+            return [list(int(x) for x in row)]
+        buf = np.zeros(self.world * k, dtype=np.uint64)
+        buf[self.rank * k:(self.rank + 1) * k] = np.asarray(row, dtype=np.uint64)
+        out = self.eng.allreduce_u64(buf)
+        return [[int(x) for x in out[r * k:(r + 1) * k]] for r in range(self.world)]
 
 
-def barrier(dist, world):
-    if world > 1:
-        dist.barrier()
-
-
-def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
+def timed_run(eng, job, steps, warmup, with_hash):
     """W untimed + K timed generations.  Returns (seconds, kernel ms,
     launches, generations covered by them, probe clock GHz, hashes): hashes
-    = the W + K per-generation partial hashes of this shard when with_hash."""
+    = the W + K per-generation partial hashes of this shard when with_hash.
+    `job`: the Job whose ranks step together, or None (this GPU alone)."""
+    ranks = job is not None and job.world > 1
     hw = eng.step(warmup, hashes=with_hash) if warmup > 0 else None
     eng.sync()
     eng.profile(True)
     eng.profile_reset()
-    barrier(dist, world)
-    torch.cuda.synchronize()
+    if ranks:
+        job.barrier()
+    eng.sync()
     t0 = time.perf_counter()
     ht = eng.step(steps, hashes=with_hash)
     eng.sync()
-    torch.cuda.synchronize()
     # the clock stops when this rank's work is done; the closing barrier and
-    # the max over ranks then give the job's time (a gloo barrier costs
-    # ~1 ms, a real share of an N = 8 rank's 20-step window)
+    # the max over ranks then give the job's time
     dt = time.perf_counter() - t0
-    barrier(dist, world)
+    if ranks:
+        job.barrier()
     kms, launches, gens = eng.profile_read()
     clock = eng.profile_clock()  # GHz the timed launches ran at (in-kernel probe)
+    timed_run.stats = eng.profile_stats()
     eng.profile(False)
-    if world > 1:
+    if ranks:
         # every rank's own time (rank order) -> the job's time is their max
-        t = torch.zeros(world, dtype=torch.float64)
-        t[dist.get_rank()] = dt
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        timed_run.rank_times = [float(x) for x in t.tolist()]
+        timed_run.rank_times = [r[0] / 1e9 for r in job.gather([round(dt * 1e9)])]
         dt = max(timed_run.rank_times)
     hashes = None
     if with_hash:
@@ -133,17 +201,18 @@ def timed_run(eng, torch, dist, world, steps, warmup, with_hash):
 GOLDEN_SEED = 0x5EED
 
 
-def golden_path(W):
-    return os.path.join("tests", "golden", f"bench_{W}.json")
+def golden_path(W, H):
+    return os.path.join("tests", "golden", f"bench_{W}.json" if W == H else f"bench_{W}x{H}.json")
 
 
 def golden_hashes(W, H):
-    """Global state hashes of the bench board (W x H torus, B3/S23, seed
-    0x5EED) at epochs 0, 1, ..., from tests/golden/bench_<W>.json -- written by
-    tests/golden/make_bench_golden.py with the CPU oracle (a data file: bench
-    never runs the oracle to check itself).  None if there is no table."""
+    """Global state hashes of a bench board (W x H torus, B3/S23, seed
+    0x5EED) at epochs 0, 1, ..., from tests/golden/bench_<W>[x<H>].json --
+    written by tests/golden/make_bench_golden.py with the CPU oracle (a data
+    file: bench never runs the oracle to check itself).  None if there is no
+    table."""
     try:
-        with open(os.path.join(ROOT, golden_path(W))) as f:
+        with open(os.path.join(ROOT, golden_path(W, H))) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
@@ -152,50 +221,59 @@ def golden_hashes(W, H):
     return [int(x, 16) for x in d["hashes"]]
 
 
-def global_hash(eng, world):
+def global_hash(eng, job):
     """The whole board's state hash: gol_hash of every shard, summed over the
     ranks with gol_comm_allreduce_u64 (RCCL) -- the hash is a sum mod 2^64, so
     the N shards' partials add up to the N = 1 value."""
     import numpy as np
     h = np.array([eng.hash()], dtype=np.uint64)
-    if world > 1:
+    if job is not None and job.world > 1:
         h = eng.allreduce_u64(h)
     return int(h[0])
 
 
 class Parity:
-    """bench.py's self-check against the committed golden hashes: every rank's
-    shard is checked at every N, so the multi-GPU line records whether the RCCL
-    halo exchange kept the board bit-exact (CellActor.scala:71-77,
-    NextStateCellGathererActor.scala:32-36 are the exchange it replaces)."""
+    """bench.py's self-check against the committed golden hashes: every board
+    it times is checked at the epoch its window ends on (the shards of every
+    rank through the summed hash at N > 1, so the multi-GPU line records
+    whether the RCCL halo exchange kept the board bit-exact;
+    CellActor.scala:71-77, NextStateCellGathererActor.scala:32-36 are the
+    exchange it replaces).  Each check is also returned, for the sub-line it
+    belongs to."""
 
-    def __init__(self, W, H):
-        self.golden = golden_hashes(W, H)
-        self.source = golden_path(W)
+    def __init__(self):
+        self.tables = {}
         self.checks = []
 
-    def _golden(self, epoch):
-        return self.golden[epoch] if self.golden is not None and epoch < len(self.golden) else None
+    def _golden(self, shape, epoch):
+        if shape not in self.tables:
+            self.tables[shape] = golden_hashes(*shape)
+        g = self.tables[shape]
+        return g[epoch] if g is not None and epoch < len(g) else None
 
-    def board(self, what, epoch, value):
-        g = self._golden(epoch)
-        self.checks.append({"what": what, "epoch": epoch, "hash": f"{value:#018x}",
-                            "golden": None if g is None else f"{g:#018x}",
-                            "match": None if g is None else value == g})
+    def board(self, what, shape, epoch, value):
+        g = self._golden(shape, epoch)
+        c = {"what": what, "board": f"{shape[0]}x{shape[1]}", "epoch": epoch, "hash": f"{value:#018x}",
+             "golden": None if g is None else f"{g:#018x}", "match": None if g is None else value == g}
+        self.checks.append(c)
+        return {k: c[k] for k in ("epoch", "hash", "golden", "match")}
 
-    def sequence(self, what, first_epoch, values):
-        gs = [self._golden(first_epoch + k) for k in range(len(values))]
+    def sequence(self, what, shape, first_epoch, values):
+        gs = [self._golden(shape, first_epoch + k) for k in range(len(values))]
         known = [(first_epoch + k, int(v), g) for k, (v, g) in enumerate(zip(values, gs)) if g is not None]
         bad = [e for e, v, g in known if v != g]
-        self.checks.append({"what": what, "epochs": [first_epoch, first_epoch + len(values) - 1],
-                            "checked": len(known), "mismatched_epochs": bad[:16],
-                            "last_hash": f"{int(values[-1]):#018x}" if len(values) else None,
-                            "match": (not bad) if known else None})
+        c = {"what": what, "board": f"{shape[0]}x{shape[1]}", "epochs": [first_epoch, first_epoch + len(values) - 1],
+             "checked": len(known), "mismatched_epochs": bad[:16],
+             "last_hash": f"{int(values[-1]):#018x}" if len(values) else None,
+             "match": (not bad) if known else None}
+        self.checks.append(c)
+        return c
 
     def report(self):
         ms = [c["match"] for c in self.checks]
-        return {"golden": f"{self.source} (CPU oracle, tests/golden/make_bench_golden.py; "
-                          "parity unpinned: the reference ships no vectors)" if self.golden else None,
+        used = sorted(golden_path(*k) for k, v in self.tables.items() if v is not None)
+        return {"golden": (", ".join(used) + " (CPU oracle, tests/golden/make_bench_golden.py; "
+                           "parity unpinned: the reference ships no vectors)") if used else None,
                 "checks": self.checks,
                 "match": None if not ms or any(m is None for m in ms) else all(ms)}
 
@@ -224,15 +302,18 @@ def _cpu_rate(O, width, H, threads, seconds):
 
 def cpu_baseline(width, seconds):
     """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
-    workload: a torus of the same width and 1024 rows, run for ~`seconds`.
-    The reported value uses the CPU share the harness grants the job
-    (OMP_NUM_THREADS: 16 threads per GPU on the pool's boxes); a shorter
-    sample on every core of sched_getaffinity (all
-    host cores) is reported beside it when that is more threads."""
+    workload: a torus of the same width and 1024 rows, run for ~`seconds`,
+    on the CPU share the harness grants the job (OMP_NUM_THREADS: 16 threads
+    per GPU on the pool's boxes; sched_getaffinity when unset).  More threads
+    than the job's cgroup quota would only time-slice on the same CPUs, so no
+    such figure is reported."""
     from oracle import oracle as O
     affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = min(share, affinity) if share > 0 else affinity
+    quota = cgroup_cpus()
+    if quota:
+        threads = max(1, min(threads, int(quota)))
     H = 1024
     v, gens, dt = _cpu_rate(O, width, H, threads, seconds)
     out = {"value": round(v, 3), "unit": "GCUPS", "cores": threads,
@@ -240,15 +321,8 @@ def cpu_baseline(width, seconds):
            "threads_source": "OMP_NUM_THREADS (the job's CPU share)" if share > 0 else "sched_getaffinity",
            "sample": f"oracle_run_packed (oracle/gol_oracle.c, bit-sliced, OpenMP), {width}x{H} torus B3/S23 "
                      f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
-    quota = cgroup_cpus()
     if quota:
         out["cgroup_cpu_quota"] = quota
-    if affinity > threads:
-        va, ga, dta = _cpu_rate(O, width, H, affinity, max(seconds / 3, 1.0))
-        out["all_affinity"] = {"value": round(va, 3), "unit": "GCUPS", "cores": affinity,
-                               "sample": f"same slice, {ga} generations in {dta:.1f} s on {affinity} threads",
-                               "note": (f"the job's cgroup grants {quota:g} CPUs: {affinity} threads time-slice on "
-                                        "them" if quota and quota < affinity else "every core of sched_getaffinity")}
     return out
 
 
@@ -387,55 +461,77 @@ def kernel_label(info, depths):
     return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE> ({waves} waves/CU resident)"
 
 
-def settle(eng, ms, with_hash, chunk):
-    """Step `eng` untimed until `ms` of GPU time has passed: after an idle
-    gap (context creation, seeding) the chip's clock dips and recovers over
-    ~15-20 ms of work (profiles/r02_warmup_curve.txt), longer than a short
-    window at 0.04 ms per generation."""
+def settle(eng, ms, chunk, job=None):
+    """Step `eng` untimed until `ms` of wall time has passed: after an idle
+    gap (context creation, seeding, a 16 GiB allocation) the chip's clock
+    dips and recovers over ~20 launches (profiles/r02_warmup_curve.txt),
+    longer than a short window.  With ranks, rank 0's clock decides when all
+    stop (every rank must step the same generations: the passes exchange
+    halos)."""
+    ranks = job is not None and job.world > 1
     t0 = time.perf_counter()
-    while (time.perf_counter() - t0) * 1e3 < ms:
-        eng.step(chunk, hashes=with_hash)
+    while True:
+        eng.step(chunk)
         eng.sync()
+        go = int((time.perf_counter() - t0) * 1e3 < ms)
+        if ranks:
+            go = int(eng.allreduce_u64([go if job.rank == 0 else 0])[0])
+        if not go:
+            return
 
 
-def secondary_run(GolEngine, torch, dist, a, local):
+def fresh_window(eng, job, steps, warmup, with_hash, settle_ms, chunk):
+    """The bench's window on a board: seed, settle (untimed), re-seed, then
+    W warm-up and K timed generations -- so the window ends at epoch W + K
+    from the seed whatever the settle did, and its hash has a golden value."""
+    if settle_ms > 0:
+        eng.seed(GOLDEN_SEED)
+        settle(eng, settle_ms, chunk, job)
+    eng.seed(GOLDEN_SEED)
+    return timed_run(eng, job, steps, warmup, with_hash)
+
+
+def secondary_run(GolEngine, a, local, parity=None):
     """BASELINE.json configs[2]: the 65536^2 single-GPU roofline run.
 
-    Two windows on the same board: SURVEY.md section 8(d)'s minimum (>= 10
-    warm-up, >= 100 timed generations: 4 ms at 65536^2, inside the clock's
-    recovery after the idle gap) as "short_window", and the reported value
-    over >= 1024 generations after 50 ms of untimed steps, when the clock has
-    settled (profiles/r02_warmup_curve.txt)."""
+    Three windows on the same board, each from the seed, each checked
+    against tests/golden/bench_65536.json at the epoch it ends on: SURVEY.md
+    section 8(d)'s minimum (>= 10 warm-up, >= 100 timed generations: 4 ms at
+    65536^2, inside the clock's recovery after the idle gap) as
+    "short_window"; the reported value over >= 1024 generations after a 50 ms
+    settle; and the same board one generation per HBM pass (the pure
+    bandwidth case, north_star: >= 70 % of peak HBM at 65536^2).
+    `parity`: where the checks go (None: not recorded)."""
     S = 65536
+    shape = (S, S)
+    chk = parity.board if parity is not None else (lambda *x: None)
     out = {"workload": "65536x65536 torus B3/S23 on 1 GPU (BASELINE.json configs[2])"}
     with GolEngine(S, S, topology="torus", rule="life", device=local) as e2:
         e2.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
-        e2.seed(0x5EED)
         n_s, w_s = max(a.steps, 102), max(a.warmup, 12)
-        dt_s, _, _, _, _, _ = timed_run(e2, torch, dist, 1, n_s, w_s, a.hash)
-        settle(e2, 50.0, a.hash, 64)
+        dt_s, _, _, _, _, _ = fresh_window(e2, None, n_s, w_s, a.hash, 0, 0)
+        p_s = chk("65536^2 short window: gol_hash after W + K", shape, n_s + w_s, e2.hash())
         n2 = max(a.steps, 1024)
-        dt2, kms2, l2, g2, c2, _ = timed_run(e2, torch, dist, 1, n2, 0, a.hash)
-        plan2 = e2.pass_plan(n2, hashes=a.hash)
-        # the same board one generation per HBM pass: the pure bandwidth case
-        # (north_star: >= 70 % of peak HBM bandwidth at 65536^2)
+        dt2, kms2, l2, g2, c2, _ = fresh_window(e2, None, n2, 0, a.hash, 50.0, 64)
+        p2 = chk("65536^2 window: gol_hash after K", shape, n2, e2.hash())
+        plan2 = e2.pass_plan(min(n2, 1024), hashes=a.hash)
         e2.set_tuning(band_rows=a.band, gens_per_pass=1)
-        e2.seed(0x5EED)
-        settle(e2, 50.0, a.hash, 16)
         n1 = max(a.steps, 256)
-        dt1, kms1, l1, g1, c1, _ = timed_run(e2, torch, dist, 1, n1, 0, a.hash)
-    shape = f"{S}x{S}"
-    r2 = roofline(kms2, l2, g2, S * S, plan2, shape, "N1", a.hash, c2)
-    r1 = roofline(kms1, l1, g1, S * S, [1] * n1, shape, "N1", a.hash, c1)
+        dt1, kms1, l1, g1, c1, _ = fresh_window(e2, None, n1, 0, a.hash, 50.0, 16)
+        p1 = chk("65536^2 single-generation passes: gol_hash after K", shape, n1, e2.hash())
+    sh = f"{S}x{S}"
+    r2 = roofline(kms2, l2, g2, S * S, plan2, sh, "N1", a.hash, c2)
+    r1 = roofline(kms1, l1, g1, S * S, [1] * n1, sh, "N1", a.hash, c1)
     out.update({
-        "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2, "warmup": "50 ms settled",
-        "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2,
+        "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2,
+        "warmup": "50 ms settled, re-seeded", "ms_per_step": round(dt2 / n2 * 1e3, 4), "roofline": r2,
+        "parity": p2,
         "short_window": {"value": round(S * S * n_s / dt_s / 1e9, 2), "unit": "GCUPS", "steps": n_s,
-                         "warmup": w_s, "ms_per_step": round(dt_s / n_s * 1e3, 4),
+                         "warmup": w_s, "ms_per_step": round(dt_s / n_s * 1e3, 4), "parity": p_s,
                          "note": "fresh seed right after context creation: inside the clock's recovery"},
         "single_generation_passes": {"value": round(S * S * n1 / dt1 / 1e9, 2), "unit": "GCUPS", "steps": n1,
-                                     "warmup": "50 ms settled", "ms_per_step": round(dt1 / n1 * 1e3, 4),
-                                     "roofline": r1,
+                                     "warmup": "50 ms settled, re-seeded", "ms_per_step": round(dt1 / n1 * 1e3, 4),
+                                     "roofline": r1, "parity": p1,
                                      # the same bytes over the wall-clock time per generation
                                      # (launch gaps included), beside the kernel-time frac
                                      "hbm_frac_from_ms_per_step": round(
@@ -443,53 +539,84 @@ def secondary_run(GolEngine, torch, dist, a, local):
     return out
 
 
-def ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H):
+def ring_stats(st, passes):
+    """The self-ring windows' exchange figures (gol_profile_stats_read)."""
+    n = max(st["exchanges"], 1)
+    return {"exchange_ms_per_pass": round(st["exchange_ms"] / n, 4),
+            "boundary_ms_per_pass": round(st["boundary_ms"] / max(st["boundary_launches"], 1), 4),
+            "halo_bytes_per_pass": round((st["halo_bytes_sent"] + st["halo_bytes_received"]) / max(passes, 1)),
+            "passes": passes}
+
+
+def ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity):
     """N = 1 only: the row-sharded (RCCL ring) schedule on this GPU, as a 1-rank
     self-ring (gol_capi.cpp one_pass: interior launch || G-row halo
     ncclSend/ncclRecv to itself, then the boundary rows on the edge stream).
     (1) the whole board, (2) one rank's shard of the N = 8 decomposition
     (262144 x 32768): what each of 8 ranks computes, without the xGMI latency
-    of a real ring.  Both after 50 ms of untimed steps: after the GPU idles
-    (here: the shard's allocation) the first ~15-20 ms of launches run 10-25 %
-    slower while the power management settles (profiles/r02_warmup_curve.txt),
-    which a few generations of a 0.08 ms-per-generation shard do not cover."""
+    of a real ring.  Every window starts from the seed and is checked against
+    its golden table (bench_262144.json, bench_262144x32768.json)."""
     out = {}
-    warm = "50 ms settled"
+    warm = "settled, re-seeded"
     eng.comm_init(N.unique_id(), 0, 1)
-    eng.seed(0x5EED)
-    settle(eng, 50.0, False, 12)
-    dt, kms, launches, gcov, _, _ = timed_run(eng, torch, dist, 1, a.steps, a.warmup, False)
-    out["whole_board_self_ring"] = {"value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS",
-                                    "warmup": warm, "ms_per_step": round(dt / a.steps * 1e3, 4),
-                                    "pass_plan": eng.pass_plan(min(a.steps, 1024))}
+    dt, kms, launches, gcov, _, _ = fresh_window(eng, None, a.steps, a.warmup, False, 100.0, 12)
+    st = timed_run.stats
+    out["whole_board_self_ring"] = {
+        "value": round(W * H * a.steps / dt / 1e9, 2), "unit": "GCUPS", "warmup": f"{a.warmup} ({warm})",
+        "ms_per_step": round(dt / a.steps * 1e3, 4), "pass_plan": eng.pass_plan(min(a.steps, 1024)),
+        "exchange": ring_stats(st, launches),
+        "parity": parity.board("whole-board self-ring: gol_hash after W + K", (W, H), a.warmup + a.steps, eng.hash())}
     rows8 = H // 8
+    shape8 = (W, rows8)
     with GolEngine(W, H, topology="torus", rule="life", device=local, row0=0, rows=rows8) as e8:
         e8.comm_init(N.unique_id(), 0, 1)  # a 1-rank ring over a shard-sized torus
         # First as an N = 8 rank meets the driver's window (main(), N > 1):
         # the GPU idle while the ranks initialise RCCL, the 65536^2 run, then
-        # seed, W warm-up steps and the timed steps, no settle -- like the
-        # N = 1 line's own window, so the two compare directly.
+        # the rank's own settle, seed, W warm-up and K timed steps.
         time.sleep(1.0)
         if not a.no_secondary:
-            secondary_run(GolEngine, torch, dist, a, local)
-        e8.seed(0x5EED)
-        dtf, _, _, _, _, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+            secondary_run(GolEngine, a, local)
+        dtf, _, _, _, _, _ = fresh_window(e8, None, a.steps, a.warmup, False, 100.0, 12)
         out["per_rank_shard_driver_window"] = {
             "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dtf / 1e9, 2),
-            "unit": "GCUPS", "warmup": a.warmup, "ms_per_step": round(dtf / a.steps * 1e3, 4),
+            "unit": "GCUPS", "warmup": f"{a.warmup} ({warm})", "ms_per_step": round(dtf / a.steps * 1e3, 4),
+            "parity": parity.board("N = 8 rank's shard, driver's sequence: gol_hash after W + K", shape8,
+                                   a.warmup + a.steps, e8.hash()),
             "note": "an N = 8 rank's sequence on this GPU (1 s idle for the communicator setup, the 65536^2 run, "
-                    "seed, W warm-up and K timed steps); x 8 / the N = 1 value is the per-cell efficiency that "
-                    "run can reach before any xGMI cost"}
-        e8.seed(0x5EED)
-        settle(e8, 50.0, False, 12)
-        dt8, kms8, l8, g8, c8, _ = timed_run(e8, torch, dist, 1, a.steps, a.warmup, False)
+                    "the same settle and re-seed as main(), W warm-up and K timed steps); x 8 / the N = 1 value "
+                    "is the per-cell efficiency that run can reach before any xGMI cost"}
+        time.sleep(1.0)
+        dt8, kms8, l8, g8, c8, _ = fresh_window(e8, None, a.steps, a.warmup, False, 100.0, 12)
+        st8 = timed_run.stats
+        p8 = parity.board("N = 8 rank's shard, self-ring: gol_hash after W + K", shape8, a.warmup + a.steps,
+                          e8.hash())
         plan8 = e8.pass_plan(min(a.steps, 1024))
     out["per_rank_shard_self_ring"] = {
         "shard": f"{W}x{rows8} (one rank of N = 8)", "value": round(W * rows8 * a.steps / dt8 / 1e9, 2),
-        "unit": "GCUPS", "warmup": warm, "ms_per_step": round(dt8 / a.steps * 1e3, 4), "pass_plan": plan8,
+        "unit": "GCUPS", "warmup": f"{a.warmup} ({warm}, after 1 s idle)", "ms_per_step": round(dt8 / a.steps * 1e3, 4),
+        "pass_plan": plan8, "exchange": ring_stats(st8, l8), "parity": p8,
         "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
                                     f"{W}x{rows8}", "ring", False, c8)}
     return out
+
+
+def lib_fingerprint(info):
+    """64-bit digest of the HIP and RCCL library paths (rank comparison)."""
+    d = hashlib.sha1((info["hip_library"] + "|" + info["rccl_library"]).encode()).digest()
+    return int.from_bytes(d[:8], "little")
+
+
+def rank_table(job, N, stats, dt, info):
+    """Every rank's diagnostics at N > 1, gathered over
+    RCCL: its window time, its interior launches, the halo exchange on its
+    comm stream, its boundary launches, halo bytes, the runtime it ran on and
+    the HIP statuses RCCL left behind in it."""
+    absorbed, _ = N.absorbed()
+    row = [round(dt * 1e9), round(stats["kernel_ms"] * 1e6), stats["launches"], round(stats["exchange_ms"] * 1e6),
+           stats["exchanges"], round(stats["boundary_ms"] * 1e6), stats["boundary_launches"],
+           stats["halo_bytes_sent"], stats["halo_bytes_received"], absorbed, info["hip_runtime_version"],
+           info["rccl_version"], lib_fingerprint(info)]
+    return job.gather(row)
 
 
 def main():
@@ -500,46 +627,45 @@ def main():
     sys.stdout.flush()
     result_fd = os.dup(1)
     os.dup2(2, 1)
-    torch, dist, rank, world, local = dist_setup(a.gpus)
+    job = Job(a.gpus)
     from gameoflife import _native as N
     from gameoflife.engine import GolEngine
+    rank, world, local = job.rank, job.world, job.local
+    info = N.runtime_info()
 
     W = H = a.board
+    parity = Parity()
     # Every GPU runs the same sequence at every N: the 65536^2 measurement
     # (BASELINE.json configs[2]) first, then the 262144^2 workload.  At N = 1
     # the 65536^2 board comes first because a board allocated after the
     # 16 GiB one was freed stepped ~5 % slower (scripts/alloc_order.py); at
     # N > 1 each rank creates its shard and its RCCL communicator first (the
     # communicator setup idles the GPU for up to a second), then runs the same
-    # 65536^2 measurement, so the sharded window starts from a GPU as busy as
-    # the N = 1 window does (after an idle gap the first ~15-20 ms of launches
-    # run 10-25 % slower, profiles/r02_warmup_curve.txt).
+    # 65536^2 measurement.  Either way the timed window then starts from its
+    # own settle (fresh_window).
     secondary = None
     if world == 1 and not a.no_secondary:
-        secondary = secondary_run(GolEngine, torch, dist, a, local)
+        secondary = secondary_run(GolEngine, a, local, parity)
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
     eng.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)
     if world > 1:
-        uid = N.unique_id() if rank == 0 else bytes(N.GOL_UNIQUE_ID_BYTES)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        eng.comm_init(bytes(t.tolist()), rank, world)
+        job.join(eng, N)
         if not a.no_secondary:
-            secondary = secondary_run(GolEngine, torch, dist, a, local)
+            secondary = secondary_run(GolEngine, a, local, parity if rank == 0 else None)
             secondary["note"] = f"measured on rank {rank}'s GPU; each of the {world} ranks ran it on its own GPU"
-    eng.seed(GOLDEN_SEED)
-    parity = Parity(W, H)
 
-    dt, kms, launches, gcov, clk, hs = timed_run(eng, torch, dist, world, a.steps, a.warmup, a.hash)
+    dt, kms, launches, gcov, clk, hs = fresh_window(eng, job, a.steps, a.warmup, a.hash, 100.0, 12)
+    stats = timed_run.stats
     e1 = a.warmup + a.steps
     rank_times = list(getattr(timed_run, "rank_times", []))
+    ranks_diag = rank_table(job, N, stats, dt if world == 1 else rank_times[rank], info) if world > 1 else None
     if hs is not None:
         parity.sequence("fused per-generation hashes of the W + K generations (global: shard partials "
                         "summed by gol_comm_allreduce_u64 at N > 1)",
-                        1, eng.allreduce_u64(hs) if world > 1 else hs)
-    parity.board("gol_hash of the board after the W + K generations (summed over the ranks)", e1,
-                 global_hash(eng, world))
+                        (W, H), 1, eng.allreduce_u64(hs) if world > 1 else hs)
+    parity.board("gol_hash of the board after the W + K generations (summed over the ranks)", (W, H), e1,
+                 global_hash(eng, job))
     eng_info = {g: eng.occupancy(g) for g in range(1, 13)}
     plan = eng.pass_plan(min(a.steps, 1024), hashes=a.hash)
     value = W * H * a.steps / dt / 1e9
@@ -549,10 +675,11 @@ def main():
         # parity contract's output: one u64 per generation),
         # continuing from the board the timed run left; at N > 1 the shards'
         # per-generation partials are summed over the ring (RCCL all-reduce)
-        dth, kmsh, lh, gh, ch, hh = timed_run(eng, torch, dist, world, a.steps, a.warmup, True)
+        dth, kmsh, lh, gh, ch, hh = timed_run(eng, job, a.steps, a.warmup, True)
         parity.sequence("fused per-generation hashes of the hashed window (global: shard partials summed "
-                        "by gol_comm_allreduce_u64 at N > 1)", e1 + 1, eng.allreduce_u64(hh) if world > 1 else hh)
-        parity.board("gol_hash of the board after the hashed window", 2 * e1, global_hash(eng, world))
+                        "by gol_comm_allreduce_u64 at N > 1)", (W, H), e1 + 1,
+                        eng.allreduce_u64(hh) if world > 1 else hh)
+        parity.board("gol_hash of the board after the hashed window", (W, H), 2 * e1, global_hash(eng, job))
         hplan = eng.pass_plan(min(a.steps, 1024), hashes=True)
         vh = W * H * a.steps / dth / 1e9
         hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
@@ -571,7 +698,13 @@ def main():
         roof["kernel"] = kernel_label(eng_info, plan)
     ring = None
     if world == 1 and not a.no_ring and not a.hash:
-        ring = ring_schedule_runs(GolEngine, N, torch, dist, a, local, eng, W, H)
+        ring = ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity)
+    absorbed, absorbed_last = N.absorbed()
+    runtime = dict(info, rccl_statuses_absorbed=absorbed)
+    if absorbed:
+        runtime["rccl_status_last"] = absorbed_last
+    if ranks_diag is not None:
+        runtime["same_on_all_ranks"] = len({tuple(r[10:13]) for r in ranks_diag}) == 1
     out = {
         "metric": "cell updates/sec (GCUPS) at 1/2/4/8 MI355X + % of HBM roofline",
         "value": round(value, 2),
@@ -591,21 +724,35 @@ def main():
                    "parallelism": ("single GPU, whole board (no halo exchange)" if world == 1 else
                                    f"row-block x{world}, G-deep RCCL halo send/recv per pass (ring over xGMI)"),
                    "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
-                   "fused_hash": bool(a.hash)},
+                   "fused_hash": bool(a.hash),
+                   "window": "seed, 100 ms untimed settle, re-seed, W warm-up + K timed generations"},
         "roofline": roof,
         "parity": parity.report(),
+        "runtime": runtime,
     }
     if world > 1:
         rt = rank_times
+        d = ranks_diag
         out["ranks"] = {"ms_per_step": [round(x / a.steps * 1e3, 4) for x in rt],
                         "rows": [N.shard_rows(H, r, world)[1] for r in range(world)],
                         "gcups": [round(W * N.shard_rows(H, r, world)[1] * a.steps / x / 1e9, 2)
                                   for r, x in enumerate(rt)],
-                        "note": "each rank's own timed window (clock stopped at its own sync); value uses the max"}
+                        "interior_ms_per_launch": [round(r[1] / 1e6 / max(r[2], 1), 4) for r in d],
+                        "exchange_ms_per_pass": [round(r[3] / 1e6 / max(r[4], 1), 4) for r in d],
+                        "boundary_ms_per_pass": [round(r[5] / 1e6 / max(r[6], 1), 4) for r in d],
+                        "halo_bytes_per_pass": [round((r[7] + r[8]) / max(r[2], 1)) for r in d],
+                        "passes": [r[2] for r in d],
+                        "rccl_statuses_absorbed": [r[9] for r in d],
+                        "hip_runtime_version": [r[10] for r in d],
+                        "rccl_version": [r[11] for r in d],
+                        "note": "each rank's own timed window (clock stopped at its own sync; value uses the max); "
+                                "interior = the launch overlapping the exchange; exchange = comm-stream HIP events "
+                                "around the RCCL group, waiting for a late peer included"}
     if hashed is not None:
         out["with_state_hash"] = hashed
     if ring is not None:
         out["ring_schedule_n1"] = ring
+    job.barrier()
     eng.close()
 
     if rank == 0 and secondary is not None:
@@ -615,8 +762,6 @@ def main():
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(out) + "\n").encode())
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

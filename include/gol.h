@@ -89,7 +89,14 @@ typedef struct gol_config {
 /* Create a shard context.  Replaces createAllInitialActors
  * (BoardCreator.scala:79-89) + CellActor construction (CellActor.scala:10,
  * 34: epochToState = Map(0 -> initialState)).  The board starts all dead at
- * epoch 0; fill it with gol_seed() or gol_load(). */
+ * epoch 0; fill it with gol_seed() or gol_load().
+ * GOL_REF_CLIPPED boards on which some cell has no visible neighbour are
+ * refused with GOL_EINVAL: the reference never completes a generation on them
+ * (such a cell's gatherer has nobody to ask, so it never commits an epoch,
+ * NextStateCellGathererActor.scala:26-27,39-58, and its neighbours' requests
+ * for that epoch queue forever, CellActor.scala:75-76,92-94).  With the
+ * default visible extents that is a board of size w = 0 or h = 0 (one cell
+ * wide or tall) or w = h = 1 (2 x 2 cells). */
 int gol_create(gol_ctx** out, const gol_config* cfg);
 
 /* Free device memory and streams.  Replaces stopping the cell actors. */
@@ -280,13 +287,65 @@ int gol_profile_reset(gol_ctx* ctx);
  * and 100 MHz reference counters at start and end (0 if none recorded). */
 int gol_profile_clock(gol_ctx* ctx, double* ghz);
 
+/* Per-rank breakdown of the profiled passes of a sharded context (the cost
+ * of the cross-backend exchange the reference carries as GetStateFromEpoch /
+ * StateForEpoch messages, CellActor.scala:71-77,
+ * NextStateCellGathererActor.scala:32-36).  Since the last
+ * gol_profile_reset, with profiling enabled:
+ *   kernel_ms / launches / generations: as gol_profile_read (the dominant
+ *       launch: the whole shard, or a sharded shard's interior rows);
+ *   exchange_ms / exchanges: the halo exchange of each sharded pass, timed by
+ *       HIP events on the comm stream around the RCCL group (or loopback
+ *       copies): from the moment the plane is final to the moment every send
+ *       and receive of the pass has completed -- waiting for a late peer
+ *       included;
+ *   boundary_ms / boundary_launches: the boundary-row launches on the edge
+ *       stream;
+ *   halo_bytes_sent / halo_bytes_received: bytes posted to / expected from
+ *       the ring's send and receive operations (counted whether or not
+ *       profiling is enabled);
+ *   clock_ghz: as gol_profile_clock. */
+typedef struct gol_profile_stats {
+    double kernel_ms;
+    uint64_t launches;
+    uint64_t generations;
+    double exchange_ms;
+    uint64_t exchanges;
+    double boundary_ms;
+    uint64_t boundary_launches;
+    uint64_t halo_bytes_sent;
+    uint64_t halo_bytes_received;
+    double clock_ghz;
+} gol_profile_stats;
+int gol_profile_stats_read(gol_ctx* ctx, gol_profile_stats* out);
+
+/* The runtime stack this process's libgol is bound to: the HIP runtime and
+ * RCCL versions it calls and the files the dynamic linker resolved them to
+ * (dladdr of a symbol of each), plus libgol's own path.  Host-only: needs no
+ * device.  A JVM host and the Python tools report the same fields, so a
+ * multi-rank run states which library stack it exercised. */
+typedef struct gol_runtime_info {
+    int32_t abi_version;
+    int32_t hip_runtime_version;  /* hipRuntimeGetVersion (0 if it failed)  */
+    int32_t hip_driver_version;   /* hipDriverGetVersion  (0 if it failed)  */
+    int32_t rccl_version;         /* ncclGetVersion, e.g. 22707 = 2.27.7    */
+    char hip_library[512];        /* path of the libamdhip64 in use         */
+    char rccl_library[512];       /* path of the librccl in use             */
+    char gol_library[512];        /* path of this libgol                    */
+} gol_runtime_info;
+int gol_runtime_info_get(gol_runtime_info* out);
+
 /* Tuning knobs (results never depend on them); 0 selects the automatic
  * choice, which is also the default of a new context:
  *   band_rows       rows of output streamed by one wave;
  *   gens_per_pass   generations fused per HBM pass (temporal blocking, 1..12;
  *                   automatic: the pass planner, see gol_pass_plan);
  *   words_per_lane  32-bit words each lane owns per row (1, 2 or 4; must
- *                   divide the words of a row). */
+ *                   divide the words of a row).
+ * GOL_EINVAL for words_per_lane = 4 together with gens_per_pass > 8 on any
+ * board but the B3/S23 torus: those kernel instances (generic rule masks,
+ * clipped visibility) would spill registers to scratch (the planner never
+ * picks them). */
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane);
 
 /* Diagnostic: the pass depths (generations fused per HBM pass) gol_step would

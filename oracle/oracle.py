@@ -275,3 +275,39 @@ def java_random_next_booleans(seed: int, n: int) -> list[bool]:
         s = (s * 0x5DEECE66D + 0xB) & mask
         out.append((s >> 47) != 0)
     return out
+
+
+def reference_commit_epochs(w: int, h: int, target: int) -> dict:
+    """The epoch each cell of the reference's (w+1) x (h+1) board has
+    committed once every message has been delivered, capped at `target`:
+    a restatement of the reference's commit condition, not of its rule.
+
+    A cell at epoch e spawns a gatherer that asks every visible neighbour
+    (package.scala:17-28) for its state at epoch e
+    (NextStateCellGathererActor.scala:26-27,32-36); a neighbour answers once it
+    holds epoch e, from its never-pruned history, and queues the request until
+    then (CellActor.scala:71-77).  The gatherer completes -- and the cell
+    commits e + 1 (:39-47, CellActor.scala:79-89) -- only when the last
+    expected answer arrives, so a cell with no visible neighbour never commits
+    (its gatherer retries, fails, and the cell re-asks for neighbours forever:
+    :49-53, CellActor.scala:92-94), and its neighbours stop one epoch after it.
+    Returns {(x, y): epoch}."""
+    cells = [(i, j) for i in range(w + 1) for j in range(h + 1)]
+    nbrs = {c: [(c[0] + di, c[1] + dj) for di in (-1, 0, 1) for dj in (-1, 0, 1)
+                if (di, dj) != (0, 0) and 0 <= c[0] + di < w and 0 <= c[1] + dj < h] for c in cells}
+    epoch = {c: 0 for c in cells}
+    changed = True
+    while changed:
+        changed = False
+        for c in cells:
+            e = epoch[c]
+            if e < target and nbrs[c] and all(epoch[n] >= e for n in nbrs[c]):
+                epoch[c] = e + 1
+                changed = True
+    return epoch
+
+
+def reference_completes(w: int, h: int, generations: int = 3) -> bool:
+    """Does the reference board of size (w, h) reach `generations` whole
+    generations (every cell committed)?  See reference_commit_epochs."""
+    return min(reference_commit_epochs(w, h, generations).values()) >= generations

@@ -12,11 +12,36 @@
 
 constexpr int kIters = 4096;
 
+// Round 4: the hg loop mix with the cross-lane move taken
+// off the VALU and / or a 4-word interleave.
+//   MODE 5: MODE 4 with the 2 DPP wave shifts replaced by ds_bpermute_b32 (LDS
+//           pipe, no LDS allocation), requested one row ahead: the words a
+//           chain needs next iteration are asked for at the end of this one.
+//   MODE 6: quad layout -- 4 words per lane, cell 4b + j in word j bit b: per
+//           quad 2 DPP + 2 v_alignbit + 8 + 4 x 7 v_bitop3 = 40 ops (MODE 4:
+//           44 for two pairs).
+//   MODE 7: MODE 6 with ds_bpermute one row ahead.
+__device__ __forceinline__ uint32_t rule7(uint32_t a0, uint32_t a1, uint32_t c0, uint32_t c1, uint32_t b0, uint32_t b1,
+                                          uint32_t alive) {
+    const uint32_t e1 = __builtin_amdgcn_bitop3_b32(a0, c0, b0, 0x69);
+    const uint32_t e2 = __builtin_amdgcn_bitop3_b32(a0, c0, b0, 0x7e);
+    const uint32_t f1 = __builtin_amdgcn_bitop3_b32(a1, c1, b1, 0x69);
+    const uint32_t f2 = __builtin_amdgcn_bitop3_b32(a1, c1, b1, 0x7e);
+    const uint32_t t1 = __builtin_amdgcn_bitop3_b32(e1, e2, f2, 0x56);
+    const uint32_t t2 = __builtin_amdgcn_bitop3_b32(e1, alive, t1, 0x45);
+    return __builtin_amdgcn_bitop3_b32(e2, f1, t2, 0x28);
+}
+
 template <int MODE, int CH>
 __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned long long* clk) {
-    uint32_t a[CH], b[CH], c[CH];
+    uint32_t a[CH], b[CH], c[CH], d[CH], pl[CH], pr[CH];
+    const int lane = threadIdx.x & 63;
+    const int addr_l = ((lane + 63) & 63) * 4, addr_r = ((lane + 1) & 63) * 4;  // ds_bpermute byte addresses
 #pragma unroll
-    for (int i = 0; i < CH; ++i) { a[i] = seed * (threadIdx.x + i); b[i] = a[i] ^ 0x9e3779b9u; c[i] = a[i] + 17u; }
+    for (int i = 0; i < CH; ++i) {
+        a[i] = seed * (threadIdx.x + i); b[i] = a[i] ^ 0x9e3779b9u; c[i] = a[i] + 17u; d[i] = b[i] * 5u;
+        pl[i] = a[i] >> 3; pr[i] = b[i] << 3;
+    }
     unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < kIters; ++it) {
 #pragma unroll
@@ -66,6 +91,37 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
                 c[i] = h0e;
                 a[i] = out2[0];
                 b[i] = out2[1];
+            } else if constexpr (MODE == 5 || MODE == 6 || MODE == 7) {
+                constexpr bool kQuad = MODE != 5, kDs = MODE != 6;
+                constexpr int K = kQuad ? 4 : 2;
+                uint32_t q[4] = {a[i], b[i], d[i], c[i] ^ a[i]};
+                uint32_t left, right;
+                if constexpr (kDs) {
+                    left = pl[i];
+                    right = pr[i];
+                } else {
+                    left = (uint32_t)__builtin_amdgcn_mov_dpp((int)q[K - 1], 0x138, 0xf, 0xf, true);
+                    right = (uint32_t)__builtin_amdgcn_mov_dpp((int)q[0], 0x130, 0xf, 0xf, true);
+                }
+                uint32_t w[4], e[4], h0[4], h1[4], o[4];
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    w[j] = j == 0 ? __builtin_amdgcn_alignbit(q[K - 1], left, 31) : q[j - 1];
+                    e[j] = j == K - 1 ? __builtin_amdgcn_alignbit(right, q[0], 1) : q[j + 1];
+                    h0[j] = __builtin_amdgcn_bitop3_b32(w[j], q[j], e[j], 0x96);
+                    h1[j] = __builtin_amdgcn_bitop3_b32(w[j], q[j], e[j], 0xe8);
+                }
+#pragma unroll
+                for (int j = 0; j < K; ++j)
+                    o[j] = rule7(c[i], c[i] ^ 0x5a5a5a5au, h0[(j + 1) % K], h1[(j + 1) % K], h0[j], h1[j], q[j]);
+                c[i] = h0[0];
+                a[i] = o[0];
+                b[i] = o[1];
+                if constexpr (kQuad) d[i] = o[2] ^ o[3];
+                if constexpr (kDs) {  // next iteration's cross-lane words, one row ahead
+                    pl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_l, (int)(kQuad ? (c[i] ^ a[i]) : b[i]));
+                    pr[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_r, (int)a[i]);
+                }
             } else {  // step-kernel mix: 1 DPP, 2 alignbit, 9 bitop3, 1 xor  (13)
                 const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[i], 0x138, 0xf, 0xf, true);
                 const uint32_t w = __builtin_amdgcn_alignbit(a[i], l, 31);
@@ -87,13 +143,14 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
     unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < CH; ++i) acc ^= a[i] ^ b[i] ^ c[i];
+    for (int i = 0; i < CH; ++i) acc ^= a[i] ^ b[i] ^ c[i] ^ d[i] ^ pl[i] ^ pr[i];
     out[blockIdx.x * 256 + threadIdx.x] = acc;
     if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
 }
 
 template <int MODE, int CH>
-int run(const char* name, int ops_per_chain_iter, int waves_per_simd, uint32_t* out, unsigned long long* clk, int cus) {
+int run(const char* name, int ops_per_chain_iter, int waves_per_simd, uint32_t* out, unsigned long long* clk, int cus,
+        int words_per_iter = 0) {
     const int blocks = cus * waves_per_simd;  // 256-thread WG = 4 waves = 1 per SIMD
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
@@ -110,8 +167,13 @@ int run(const char* name, int ops_per_chain_iter, int waves_per_simd, uint32_t* 
     const double ghz = (double)h[0] / (double)h[1] * 0.1;  // memrealtime = 100 MHz
     const double wave_instr = (double)blocks * 4 * kIters * CH * ops_per_chain_iter;
     const double per_simd_per_cycle = wave_instr / (cus * 4.0) / (best * 1e-3 * ghz * 1e9);
-    printf("%-28s waves/SIMD=%d chains=%2d  %.3f ms  clk=%.2f GHz  wave-VALU/cycle/SIMD=%.3f  lane-ops/s=%.1fT\n", name,
+    printf("%-28s waves/SIMD=%d chains=%2d  %.3f ms  clk=%.2f GHz  wave-VALU/cycle/SIMD=%.3f  lane-ops/s=%.1fT", name,
            waves_per_simd, CH, best, ghz, per_simd_per_cycle, wave_instr * 64 / (best * 1e-3) / 1e12);
+    if (words_per_iter) {
+        const double wg = (double)blocks * 4 * kIters * CH * words_per_iter;  // wave word-generations
+        printf("  word-gen/cycle/SIMD=%.4f", wg / (cus * 4.0) / (best * 1e-3 * ghz * 1e9));
+    }
+    printf("\n");
     return 0;
 }
 
@@ -120,6 +182,21 @@ int main() {
     uint32_t* out; unsigned long long* clk;
     CHK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4)); CHK(hipMalloc(&clk, 16));
     const bool r3 = getenv("VALU_RATE_R3") != nullptr;  // only the round-3 loop mix, at 1..8 waves/SIMD
+    if (getenv("VALU_RATE_R4")) {
+        // word-generations per cycle per SIMD: a pair iteration advances 2
+        // words, a quad iteration 4 (the ops column counts VALU only)
+        for (int w : {1, 2, 3, 4, 6}) {
+            run<4, 2>("R4 pair DPP (22 VALU/pair)", 22, w, out, clk, cus, 2);
+            run<4, 4>("R4 pair DPP (22 VALU/pair)", 22, w, out, clk, cus, 2);
+            run<5, 2>("R4 pair bpermute (20 VALU)", 20, w, out, clk, cus, 2);
+            run<5, 4>("R4 pair bpermute (20 VALU)", 20, w, out, clk, cus, 2);
+            run<6, 2>("R4 quad DPP (40 VALU/quad)", 40, w, out, clk, cus, 4);
+            run<6, 4>("R4 quad DPP (40 VALU/quad)", 40, w, out, clk, cus, 4);
+            run<7, 2>("R4 quad bpermute (38 VALU)", 38, w, out, clk, cus, 4);
+            run<7, 4>("R4 quad bpermute (38 VALU)", 38, w, out, clk, cus, 4);
+        }
+        return 0;
+    }
     for (int w : {1, 2, 3, 4, 5, 6, 8}) {
         if (r3) {
             run<4, 2>("hg loop mix (22 ops/pair)", 22, w, out, clk, cus);

@@ -1,11 +1,14 @@
 """Runs bench.py's main() with a stand-in for libgol (test infrastructure for
 tests/test_bench_multirank.py, not a test module).
 
-The N > 1 control flow of bench.py -- gloo process group, communicator-id
-broadcast, barriers, max-over-ranks time, the per-rank 65536^2 run, the one
-JSON line on rank 0 -- only runs for real on the driver's multi-GPU node.
-This runner replaces the native engine by a recorder so that flow can run on
-CPU ranks: every engine call is appended to $FAKE_LOG_DIR/rank<r>.log.
+The N > 1 control flow of bench.py -- the communicator id passed through the
+rendezvous file, barriers, the settle loop, max-over-ranks time, the per-rank
+diagnostics gathered over the ring, the per-rank 65536^2 run, the one JSON
+line on rank 0 -- only runs for real on the driver's multi-GPU node.  This
+runner replaces the native engine by a recorder so that flow can run on CPU
+ranks: every engine call is appended to $FAKE_LOG_DIR/rank<r>.log, and the
+engine's all-reduce (gol_comm_allreduce_u64 over RCCL in bench.py) runs over
+a gloo process group the runner creates -- bench.py itself imports no torch.
 
     RANK=.. WORLD_SIZE=.. MASTER_ADDR=127.0.0.1 MASTER_PORT=.. FAKE_LOG_DIR=.. \
         python tests/bench_fake_runner.py --gpus N --steps K --warmup W ...
@@ -30,8 +33,9 @@ def log(*parts):
 M64 = (1 << 64) - 1
 
 
-def golden(width):
-    with open(os.path.join(ROOT, "tests", "golden", f"bench_{width}.json")) as f:
+def golden(width, height):
+    name = f"bench_{width}.json" if width == height else f"bench_{width}x{height}.json"
+    with open(os.path.join(ROOT, "tests", "golden", name)) as f:
         return [int(x, 16) for x in json.load(f)["hashes"]]
 
 
@@ -51,7 +55,7 @@ class FakeEngine:
     def _share(self, epoch):
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if self.whole or world == 1:
-            g = golden(self.w)
+            g = golden(self.w, self.rows)
             return g[epoch] if epoch < len(g) else 0
         others = [(0x9E3779B97F4A7C15 * (epoch + 1) * (r + 7)) & M64 for r in range(1, world)]
         if RANK > 0:
@@ -59,7 +63,7 @@ class FakeEngine:
             # (a halo-exchange bug), which the summed hash must expose
             bad = os.environ.get("FAKE_CORRUPT_RANK") == str(RANK) and epoch >= 20
             return (others[RANK - 1] + (1 if bad else 0)) & M64
-        g = golden(self.w)
+        g = golden(self.w, self.h)
         return ((g[epoch] if epoch < len(g) else 0) - sum(others)) & M64
 
     def hash(self):
@@ -129,6 +133,17 @@ class FakeEngine:
     def profile_clock(self):
         return 2.0 if self.launches else 0.0
 
+    def profile_stats(self):
+        sharded = not self.whole
+        return {"kernel_ms": self.ms, "launches": self.launches, "generations": self.gens,
+                "exchange_ms": 0.05 * self.launches if sharded else 0.0,
+                "exchanges": self.launches if sharded else 0,
+                "boundary_ms": 0.01 * self.launches if sharded else 0.0,
+                "boundary_launches": self.launches if sharded else 0,
+                "halo_bytes_sent": 2 * 12 * self.w // 8 * self.launches if sharded else 0,
+                "halo_bytes_received": 2 * 12 * self.w // 8 * self.launches if sharded else 0,
+                "clock_ghz": 2.0}
+
     def occupancy(self, g):
         return (12 if g > 8 else 16), 124
 
@@ -143,14 +158,28 @@ def install():
         return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
     native.shard_rows = shard_rows
+    native.runtime_info = lambda: {"hip_runtime_version": 70226015, "hip_runtime": "7.2.26015",
+                                   "hip_driver_version": 70226015, "rccl_version": 22707, "rccl": "2.27.7",
+                                   "hip_library": "/opt/rocm/lib/libamdhip64.so.7",
+                                   "rccl_library": "/opt/rocm/lib/librccl.so.1", "gol_library": "fake",
+                                   "torch_loaded": "torch" in sys.modules}
+    native.absorbed = lambda: (0, "")
     engine = types.ModuleType("gameoflife.engine")
     engine.GolEngine = FakeEngine
     pkg = types.ModuleType("gameoflife")
     pkg._native, pkg.engine = native, engine
     sys.modules.update({"gameoflife": pkg, "gameoflife._native": native, "gameoflife.engine": engine})
-    import torch
-    torch.cuda.set_device = lambda d: log("set_device", d)
-    torch.cuda.synchronize = lambda *a: None
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:  # the stand-in for the engine's RCCL all-reduce
+        import torch.distributed as dist
+        saved = os.dup(1)  # gloo's connection banner goes to fd 1: keep stdout for the JSON line
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=RANK, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
 
 if __name__ == "__main__":

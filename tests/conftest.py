@@ -29,6 +29,15 @@ def _ensure_built():
 
 _ensure_built()
 
+# Load libgol before any test module can import torch: the dynamic linker
+# then binds libgol -- and anything loaded later that asks for the same
+# sonames -- to /opt/rocm's HIP runtime and RCCL, the stack bench.py (which
+# imports no torch) and a JVM host run on.  The terminal summary names it.
+try:
+    from gameoflife import _native as _gol_native  # noqa: F401
+except ImportError:
+    _gol_native = None
+
 
 def _gpu_available() -> bool:
     try:
@@ -46,10 +55,17 @@ def gpu():
 
 
 def pytest_terminal_summary(terminalreporter):
-    """GPU runs: how many HIP statuses RCCL calls left behind during the
-    session (libgol absorbs and counts them)."""
+    """The HIP runtime and RCCL libgol ran on (gol_runtime_info_get) and, on
+    GPU runs, how many HIP statuses RCCL calls left behind during the session
+    (libgol absorbs and counts them)."""
     mod = sys.modules.get("gameoflife._native")
-    if mod is None or not _gpu_available():
+    if mod is None:
+        return
+    info = mod.runtime_info()
+    terminalreporter.write_line(
+        f"libgol runtime: HIP {info['hip_runtime']} ({info['hip_library']}), RCCL {info['rccl']} "
+        f"({info['rccl_library']}), torch loaded in this session: {info['torch_loaded']}")
+    if not _gpu_available():
         return
     n, last = mod.absorbed()
     terminalreporter.write_line(f"libgol: HIP statuses absorbed after RCCL calls this session: {n}"

@@ -1,5 +1,17 @@
-"""Generate tests/golden/bench_<W>.json: the global state hash of bench.py's
-workload board after every generation, from the CPU oracle.
+"""Generate tests/golden/bench_<W>.json (square boards) or
+bench_<W>x<H>.json: the global state hash of one of bench.py's boards after
+every generation, from the CPU oracle.
+
+Tables committed (every board bench.py times carries a parity check):
+  bench_262144.json        the headline 262144^2 board (and its N-rank shards,
+                           and the whole-board self-ring window), epochs 0..140
+  bench_65536.json         the 65536^2 roofline board (configs[2]): its short
+                           window, the 1024-generation window and the
+                           single-generation-pass window, epochs 0..1100
+  bench_262144x32768.json  one rank's shard of the N = 8 decomposition as a
+                           1-rank self-ring (a 262144 x 32768 torus; the
+                           seed is counter-based on the global row, so its
+                           rows are the big board's first 32768), epochs 0..140
 
 bench.py's headline workload is the W x W torus, B3/S23, seeded with the
 splitmix64 board of seed 0x5EED (BASELINE.json configs[3]).  The hash is
@@ -15,7 +27,7 @@ cross-checked against the independent numpy restatement (oracle.np_seed,
 oracle.np_hash) on row blocks of the board at epoch 0 and at the last epoch
 (the hash is a sum over rows, so block hashes add up to the board's).
 
-    python tests/golden/make_bench_golden.py [--board 262144] [--gens 140] [--threads 8]
+    python tests/golden/make_bench_golden.py [--board 262144] [--height H] [--gens 140] [--threads 8]
 
 262144^2 needs 16 GiB of host memory (two 8 GiB planes) and ~25 min on 8
 cores for 140 generations.
@@ -50,11 +62,14 @@ def block_check(board: np.ndarray, W: int, rows: list[int], n: int = 64) -> None
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--board", type=int, default=262144)
+    ap.add_argument("--height", type=int, default=0, help="rows (0: square board)")
     ap.add_argument("--gens", type=int, default=140)
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     a = ap.parse_args()
-    W = H = a.board
-    out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"bench_{W}.json")
+    W = a.board
+    H = a.height or a.board
+    name = f"bench_{W}.json" if H == W else f"bench_{W}x{H}.json"
+    out_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), name)
     ww = O.wwords(W)
     L = O.lib()
 

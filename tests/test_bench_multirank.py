@@ -1,8 +1,10 @@
-"""bench.py's N > 1 path on CPU ranks (gloo) with the native engine replaced
-by a recorder (tests/bench_fake_runner.py): the path the driver's multi-GPU
-scaling run takes -- communicator-id broadcast, each rank's shard, the same
-65536^2 run on every rank after its communicator exists, barriers, the
-max-over-ranks time and one JSON line from rank 0 only."""
+"""bench.py's N > 1 path on CPU ranks with the native engine replaced by a
+recorder (tests/bench_fake_runner.py; its all-reduce runs over gloo): the
+path the driver's multi-GPU scaling run takes -- the communicator id through
+the rendezvous file, each rank's shard, the same 65536^2 run on every rank
+after its communicator exists, the settle loop every rank leaves together,
+barriers, the max-over-ranks time, the per-rank diagnostics and one JSON line
+from rank 0 only.  bench.py itself never imports torch."""
 import json
 import os
 import socket
@@ -53,6 +55,7 @@ def test_multirank_bench_line(tmp_path, world):
     assert len(rk["ms_per_step"]) == world and sum(rk["rows"]) == 262144
     assert abs(max(rk["ms_per_step"]) - d["ms_per_step"]) < 1e-3
     uids = set()
+    settle_steps = []
     H = 262144
     for r, log in enumerate(logs):
         ev = [ln.split()[0] for ln in log]
@@ -67,23 +70,41 @@ def test_multirank_bench_line(tmp_path, world):
         uids.add(next(ln for ln in log if ln.startswith("comm_init")).split()[1])
         comm = next(ln for ln in log if ln.startswith("comm_init")).split()
         assert comm[2:] == [str(r), str(world)]
-        # W warm-up then exactly K timed generations on the shard
-        shard_steps = [int(ln.split()[2]) for ln in log if ln.startswith(f"step 262144x{rows} ")]
-        assert shard_steps[:2] == [5, 20]
-        # then the hashed window (W + K more generations with hashes), and each
-        # rank's shard hash goes through the all-reduce
-        assert [ln.split()[2:] for ln in log if ln.startswith(f"step 262144x{rows} ")][2:4] == \
-            [["5", "hashes"], ["20", "hashes"]]
+        # seed, an untimed settle (12-generation steps), re-seed, then W
+        # warm-up and exactly K timed generations on the shard, then the
+        # hashed window (W + K more with hashes)
+        shard = [ln for ln in log if ln.startswith(f"step 262144x{rows} ") or ln.startswith(f"seed 262144x{rows}")]
+        last_seed = max(i for i, ln in enumerate(shard) if ln.startswith("seed"))
+        assert [ln.split()[0] for ln in shard[:2]] == ["seed", "step"] and shard[1].split()[2] == "12"
+        assert [ln.split()[2:] for ln in shard[last_seed + 1:]] == [["5"], ["20"], ["5", "hashes"], ["20", "hashes"]]
+        # each rank's shard hash goes through the all-reduce
         assert [ln.split()[2] for ln in log if ln.startswith(f"hash 262144x{rows}")] == ["25", "50"]
-        assert sum(1 for ln in log if ln.startswith("allreduce")) == 3
+        # every rank left the settle loop after the same number of steps
+        settle_steps.append(sum(1 for ln in shard[:last_seed] if ln.startswith("step")))
+        assert not any(ln.startswith("set_device") for ln in log)
     assert len(uids) == 1  # every rank joined rank 0's communicator id
+    assert len(set(settle_steps)) == 1 and settle_steps[0] >= 1
+    # per-rank diagnostics gathered over the ring
+    for key in ("interior_ms_per_launch", "exchange_ms_per_pass", "boundary_ms_per_pass", "halo_bytes_per_pass",
+                "passes", "rccl_statuses_absorbed", "hip_runtime_version", "rccl_version"):
+        assert len(rk[key]) == world, key
+    assert rk["halo_bytes_per_pass"] == [2 * 2 * 12 * 262144 // 8] * world
+    assert rk["exchange_ms_per_pass"] == [0.05] * world and rk["rccl_statuses_absorbed"] == [0] * world
+    rt = d["runtime"]
+    assert rt["same_on_all_ranks"] is True and rt["rccl_library"].startswith("/opt/rocm")
+    assert rt["torch_loaded"] is False or world > 1  # the fake's all-reduce is gloo
     # parity vs tests/golden/bench_262144.json: only the sum over the ranks
     # of the shard hashes equals the golden value
     par = d["parity"]
     assert par["match"] is True, par
-    whats = [(c.get("epoch"), c.get("epochs")) for c in par["checks"]]
-    assert whats == [(25, None), (None, [26, 50]), (50, None)]
-    assert par["checks"][1]["checked"] == 25
+    whats = [(c["board"], c.get("epoch"), c.get("epochs")) for c in par["checks"]]
+    # rank 0's 65536^2 windows (short, 1024-generation, single-generation passes), then the headline
+    assert whats == [("65536x65536", 114, None), ("65536x65536", 1024, None), ("65536x65536", 256, None),
+                     ("262144x262144", 25, None), ("262144x262144", None, [26, 50]), ("262144x262144", 50, None)]
+    assert par["checks"][4]["checked"] == 25
+    assert d["secondary"]["parity"]["match"] is True
+    assert d["secondary"]["short_window"]["parity"]["epoch"] == 114
+    assert d["secondary"]["single_generation_passes"]["parity"]["match"] is True
 
 
 def test_multirank_bench_flags_a_wrong_shard(tmp_path):
@@ -105,8 +126,26 @@ def test_single_rank_keeps_cpu_baseline_slot(tmp_path):
     outs, logs = _run(1, tmp_path, "--steps", "12", "--warmup", "2", "--no-cpu", "--no-ring")
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and "note" not in d["secondary"]
-    assert d["parity"]["match"] is True and d["parity"]["checks"][0]["epoch"] == 14
+    assert d["parity"]["match"] is True
+    assert [c.get("epoch") for c in d["parity"]["checks"] if c["board"] == "262144x262144"][0] == 14
+    assert "ranks" not in d and d["runtime"]["torch_loaded"] is False
     log = logs[0]
     i_sec = next(i for i, ln in enumerate(log) if ln.startswith("create 65536x65536"))
     i_main = next(i for i, ln in enumerate(log) if ln.startswith("create 262144x262144"))
     assert i_sec < i_main and not any(ln.startswith("comm_init") for ln in log)
+
+
+def test_single_rank_ring_windows_carry_parity(tmp_path):
+    """N = 1 with the self-ring windows: the whole-board and the N = 8
+    shard's windows (driver's sequence and settled) end at epoch W + K from
+    the seed and are checked against bench_262144.json and
+    bench_262144x32768.json; a wrong shard hash would show on its sub-line."""
+    outs, logs = _run(1, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu")
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    ring = d["ring_schedule_n1"]
+    for k in ("whole_board_self_ring", "per_rank_shard_driver_window", "per_rank_shard_self_ring"):
+        assert ring[k]["parity"]["epoch"] == 25 and ring[k]["parity"]["match"] is True, k
+    assert ring["per_rank_shard_self_ring"]["exchange"]["passes"] >= 1
+    boards = {c["board"] for c in d["parity"]["checks"]}
+    assert boards == {"65536x65536", "262144x262144", "262144x32768"}
+    assert d["parity"]["match"] is True

@@ -113,3 +113,42 @@ def test_pair_layout_rule_matches_oracle():
     for w in (32, 64, 96, 128, 320, 352, 992, 1024, 4096, 65536, 262144):
         assert N.pair_layout(w) == O.pair_layout(w, O.TORUS)
         assert not N.pair_layout(w, N.GOL_REF_CLIPPED) and not O.pair_layout(w, O.REF_CLIPPED)
+
+
+def test_new_struct_layouts_match_header(tmp_path):
+    """gol_profile_stats and gol_runtime_info: ctypes mirrors match the C
+    layout (a JNI / Panama binding would read the same offsets)."""
+    src = tmp_path / "sz2.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gol.h"\n'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(gol_profile_stats),'
+                   ' offsetof(gol_profile_stats, exchange_ms), offsetof(gol_profile_stats, clock_ghz),'
+                   ' sizeof(gol_runtime_info), offsetof(gol_runtime_info, rccl_library),'
+                   ' offsetof(gol_runtime_info, gol_library)); return 0;}\n')
+    exe = tmp_path / "sz2"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    assert got == [ctypes.sizeof(N.GolProfileStats), N.GolProfileStats.exchange_ms.offset,
+                   N.GolProfileStats.clock_ghz.offset, ctypes.sizeof(N.GolRuntimeInfo),
+                   N.GolRuntimeInfo.rccl_library.offset, N.GolRuntimeInfo.gol_library.offset]
+
+
+def test_runtime_info_names_the_rocm_stack():
+    """gol_runtime_info_get is host-only: the HIP runtime and RCCL libgol is
+    bound to, and where they were loaded from.  In a process that loaded
+    libgol before torch (bench.py imports no torch; tests/conftest.py loads
+    libgol first) that is /opt/rocm's stack."""
+    info = N.runtime_info()
+    assert info["hip_library"].startswith("/opt/rocm") and "libamdhip64" in info["hip_library"]
+    assert info["rccl_library"].startswith("/opt/rocm") and "librccl" in info["rccl_library"]
+    assert info["gol_library"].endswith("libgol.so")
+    assert info["rccl_version"] >= 22000 and info["rccl"].count(".") == 2
+    assert info["hip_runtime_version"] > 0
+
+
+def test_bench_imports_no_torch():
+    """bench.py runs without torch: importing it and
+    building its argument parser leaves torch unloaded."""
+    code = ("import sys; sys.argv=['bench.py']; import bench; bench.parse(); "
+            "print('torch' in sys.modules)")
+    out = subprocess.run([os.sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "False"

@@ -94,7 +94,9 @@ def test_fault_kill_and_respawn_hashes_match(gpu, tmp_path, ckpt_dir, mode):
     sim = ShardedSimulation(W, H, 8, devices, checkpoint_every=10,
                             checkpoint_dir=str(tmp_path) if ckpt_dir else None)
     got = sim.step(25)
-    sim.kill(3)
+    # the checkpoint of epoch 20 has landed (explicit: whether an in-flight
+    # copy has reached host memory is timing on a live in-process shard)
+    sim.kill(3, checkpoint_landed=True)
     with pytest.raises(RuntimeError):
         sim.step(1)
     replayed = sim.respawn(3, mode=mode)

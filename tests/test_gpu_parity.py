@@ -142,10 +142,30 @@ def test_torus_named_rules(gpu, name, gpp):
 def test_words_per_lane(gpu, vec, gpp):
     # every lane width at every depth, full and partial strips, torus and clipped
     check_run(32 * 520, 37, 9, O.LIFE, "torus", seed=vec, gpp=gpp, vec=vec)
-    check_run(32 * 12, 29, 9, (0x0C8, 0x1A6), "torus", seed=vec, gpp=gpp, vec=vec)
     rng = np.random.default_rng(vec * 10 + gpp)
     cells = (rng.random((31, 32 * 132 - 9)) < 0.5).astype(np.uint8)
+    if vec == 4 and gpp > 7:
+        # the 16-byte-lane generic-rule / clipped instances deeper than 7
+        # would spill to scratch: gol_set_tuning refuses them
+        from gameoflife import _native as N
+        for W, topo in ((32 * 12, "torus"), (32 * 132 - 9, "ref-clipped")):
+            with engine(W, 29, topology=topo, rule=rule_obj((0x0C8, 0x1A6))) as e:
+                with pytest.raises(N.GolError) as ei:
+                    e.set_tuning(gens_per_pass=gpp, words_per_lane=vec)
+                assert ei.value.code == N.GOL_EINVAL
+        return
+    check_run(32 * 12, 29, 9, (0x0C8, 0x1A6), "torus", seed=vec, gpp=gpp, vec=vec)
     check_run(32 * 132 - 9, 31, 9, O.LIFE, "ref-clipped", cells=cells, gpp=gpp, vec=vec)
+
+
+def test_words_per_lane_4_planner_caps_generic_depth(gpu):
+    # 16-byte lanes forced with automatic depth: the planner keeps the generic
+    # and clipped instances at <= 7 generations per pass (no scratch spills)
+    with engine(32 * 12, 29, topology="torus", rule=rule_obj((0x0C8, 0x1A6))) as e:
+        e.set_tuning(words_per_lane=4)
+        assert max(e.pass_plan(60)) <= 7 and max(e.pass_plan(60, hashes=True)) <= 7
+    check_run(32 * 132 - 9, 31, 20, O.LIFE, "ref-clipped",
+              cells=(np.random.default_rng(5).random((31, 32 * 132 - 9)) < 0.5).astype(np.uint8), gpp=0, vec=4)
 
 
 @pytest.mark.parametrize("vec", [1, 2, 4])
@@ -183,7 +203,8 @@ def test_gens_not_multiple_of_depth(gpu, gpp):
         check_run(32 * 300, 45, gens, O.LIFE, "torus", seed=gens, gpp=gpp)
 
 
-CLIPPED_SHAPES = [(7, 7), (2, 2), (33, 40), (100, 65), (32, 9), (1000, 37), (32 * 300 + 5, 12),
+# (2, 2) and one-cell-wide boards are refused (tests/test_degenerate_geometry.py)
+CLIPPED_SHAPES = [(7, 7), (2, 3), (3, 2), (33, 40), (100, 65), (32, 9), (1000, 37), (32 * 300 + 5, 12),
                   (64 * 32 + 1, 20)]
 
 
@@ -202,6 +223,8 @@ def test_ref_clipped_random_rules(gpu, gpp):
     for _ in range(6):
         rule = (int(rng.integers(0, 512)), int(rng.integers(0, 512)))
         W, H = int(rng.integers(2, 400)), int(rng.integers(2, 60))
+        if W == H == 2:
+            continue  # refused: the reference stalls (tests/test_degenerate_geometry.py)
         cells = (rng.random((H, W)) < 0.5).astype(np.uint8)
         check_run(W, H, 5, rule, "ref-clipped", cells=cells, gpp=gpp)
 

@@ -14,9 +14,6 @@ import socket
 
 import numpy as np
 import pytest
-import torch
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 from gameoflife.shard import HaloPlan, combine_hashes, fixed_depth_plan, ring_depth_cap, shard_rows_py
 from oracle import oracle as O
@@ -35,6 +32,8 @@ def _free_port():
 def _exchange(plan: HaloPlan, shard: np.ndarray, G: int):
     """Issue the plan's ops as gloo isend/irecv (one 'group'): messages of G
     rows, exactly the G * pitch slices libgol sends."""
+    import torch
+    import torch.distributed as dist
     reqs, recv = [], {}
     zero = np.zeros((G, shard.shape[1]), dtype=np.uint32)
     for kind, what, peer in plan.ops():
@@ -53,6 +52,11 @@ def _exchange(plan: HaloPlan, shard: np.ndarray, G: int):
 
 
 def _worker(rank, world, port, torus, gpp, out_q):
+    # torch is imported here, not at module level: the GPU session collects
+    # this module too, and libgol must be the first to bind the HIP runtime
+    # (tests/conftest.py)
+    import torch
+    import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -91,6 +95,7 @@ def _worker(rank, world, port, torus, gpp, out_q):
 @pytest.mark.parametrize("world,torus,gpp", [(2, True, 1), (2, True, 8), (3, True, 6), (3, True, 8),
                                              (2, False, 3), (3, False, 8), (2, True, 12), (3, True, 12)])
 def test_sharded_matches_unsharded(world, torus, gpp):
+    import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
