@@ -68,7 +68,7 @@ struct gol_ctx {
     int32_t topology = GOL_TORUS;
     uint32_t birth = 0, survive = 0;
     int64_t vis_w = 0, vis_h = 0;
-    bool pairs = false;  // device words pair-interleaved (torus, even words per row)
+    int ilv = 1;         // device words per interleave group: 1 row-major, 2 pairs, 4 quads
     int device = 0;
     int vec_fixed = 0;  // words per lane forced by gol_set_tuning (0: per-pass automatic)
     // device state
@@ -340,6 +340,30 @@ EventPair* next_event_pair(gol_ctx* ctx) {
 // Automatic tuning (scripts/tune.py sweeps on MI355X, profiles/r01_*):
 // results never depend on these choices.
 
+// Device layout of a board: words per interleave
+// group.  Tori keep their columns interleaved so the stencil needs fewer
+// funnel shifts: pairs (one v_alignbit and one DPP move per word and
+// generation) where a row holds whole pairs; clipped boards stay row-major
+// (any width).  GOL_LAYOUT=quads makes tori that hold whole quads
+// quad-interleaved (one of each per two words, 16-byte lanes at 2 waves per
+// SIMD): the round-4 experiment, slower than pairs on MI355X (DESIGN.md
+// section 4 "Quad layout"), kept as an opt-in, tested layout.  The state
+// hash is defined over the device words, so the oracle follows the same
+// switch (oracle_device_ilv) and the golden tables hold pair-layout hashes.
+bool quads_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("GOL_LAYOUT");
+        return e && strcmp(e, "quads") == 0;
+    }();
+    return on;
+}
+
+int device_ilv(int32_t topology, int64_t wwords) {
+    if (topology != GOL_TORUS) return 1;
+    if (wwords % 4 == 0 && quads_enabled()) return 4;
+    return wwords % 2 == 0 ? 2 : 1;
+}
+
 // Multi-generation kernel formulation (gol_stencil.h): 1 = vertical-first,
 // 2 = horizontal-first (default: ~13.5 instead of ~15.4 VALU per word and
 // generation; +9 % at 262144^2, +24 % at 65536^2, profiles/r01_variant_ab.txt).
@@ -380,9 +404,14 @@ int xcd_chunk(int gens, int strips) {
     return std::min(64, std::max(kDefaultXcdChunk, 4 * blocks_per_band));
 }
 
-// Kernel formulation a pass at `vec` words per lane actually runs: 16-byte
-// lanes always use the vertical-first kernel (gol_stencil.h kHgLanes).
-int kernel_variant(int vec) { return vec == 4 ? 1 : stencil_variant(); }
+// Kernel formulation a pass of `gens` generations at `vec` words per lane
+// actually runs: 16-byte lanes use the vertical-first kernel, except B3/S23
+// on the quad layout up to gol::kMaxGensQuadHg generations per pass (deeper
+// rings spill; gol_stencil.h kHgLanes).
+int kernel_variant(const gol_ctx* ctx, int vec, bool life, int gens) {
+    if (vec == 4) return (ctx->ilv == 4 && life && gens <= gol::kMaxGensQuadHg) ? stencil_variant() : 1;
+    return stencil_variant();
+}
 
 // Words per lane for a single-generation pass: 16-byte lane loads where the
 // row fills whole waves of them.
@@ -394,10 +423,12 @@ int default_vec(int64_t wwords) {
 // carry 62 output lanes, so a row of w words needs ceil(w / (62 v)) strips;
 // prefer 16-byte lanes unless 8-byte lanes waste clearly fewer lanes.
 int lane_words(const gol_ctx* ctx, int gens) {
-    // the pair layout needs whole pairs per lane: 8- or 16-byte lanes
-    if (ctx->vec_fixed > 0) return ctx->pairs ? std::max(ctx->vec_fixed, 2) : ctx->vec_fixed;
+    // an interleaved layout needs whole groups per lane: pairs 8- or 16-byte
+    // lanes, quads 16-byte lanes
+    if (ctx->vec_fixed > 0) return std::max(ctx->vec_fixed, ctx->ilv);
     const int64_t w = ctx->wwords;
-    if (gens == 1) return ctx->pairs ? std::max(default_vec(w), 2) : default_vec(w);
+    if (ctx->ilv == 4) return 4;
+    if (gens == 1) return ctx->ilv == 2 ? std::max(default_vec(w), 2) : default_vec(w);
     auto util = [&](int v) -> double {
         const int64_t strips = (w / v + 61) / 62;
         return (double)(w / v) / (double)(strips * 64);
@@ -405,9 +436,9 @@ int lane_words(const gol_ctx* ctx, int gens) {
     const bool ok4 = w % 4 == 0 && w >= 4 * 62, ok2 = w % 2 == 0 && w >= 2 * 62;
     // the horizontal-first kernel keeps 3 planes per ring row: 8-byte lanes
     // (95 VGPRs at G = 6, 5 waves/SIMD) beat 16-byte lanes (183 VGPRs, 2 waves)
-    if (stencil_variant() == 2) return ok2 || ctx->pairs ? 2 : 1;
+    if (stencil_variant() == 2) return ok2 || ctx->ilv == 2 ? 2 : 1;
     if (ok4 && (!ok2 || util(4) >= util(2) - 0.03)) return 4;
-    if (ok2 || ctx->pairs) return 2;
+    if (ok2 || ctx->ilv == 2) return 2;
     return 1;
 }
 
@@ -538,12 +569,12 @@ TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int
 
 // Resident waves on the whole GPU for a launch (cached occupancy query).
 int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
-    const int variant = kernel_variant(vec);
+    const int variant = kernel_variant(ctx, vec, life, gens);
     const int key = (((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
-                     variant) * 2 + (ctx->pairs ? 1 : 0);
+                     variant) * 8 + ctx->ilv;
     auto it = ctx->occupancy_cache.find(key);
     if (it != ctx->occupancy_cache.end()) return it->second;
-    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped, ctx->pairs);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped, ctx->ilv);
     const int64_t waves = (int64_t)blocks * gol::kWavesPerWG * ctx->num_cus;
     ctx->occupancy_cache[key] = waves;
     return waves;
@@ -617,7 +648,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
     p.birth = ctx->birth;
     p.survive = ctx->survive;
-    p.variant = kernel_variant(vec);
+    p.variant = kernel_variant(ctx, vec, life, gens);
     p.xcd_chunk = xcd_chunk(gens, p.strips);
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
@@ -632,7 +663,7 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
         }
         HIP_CHECK(ctx, hipEventRecord(ev->start, stream));
     }
-    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->pairs, gx, 1, stream));
+    HIP_CHECK(ctx, gol::launch_step(p, vec, gens, life, slots != nullptr, clipped, ctx->ilv, gx, 1, stream));
     if (ev) {
         HIP_CHECK(ctx, hipEventRecord(ev->stop, stream));
         if (prof_kind == kProfMain) ctx->prof_gens += (uint64_t)gens;
@@ -1094,9 +1125,11 @@ int depth_cap(const gol_ctx* ctx) {
     int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass
                                        : (life_torus(ctx) ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
-    // 16-byte lanes forced by tuning: the generic-rule / clipped instances
-    // deeper than this spill (gol_set_tuning refuses them as fixed depths)
-    if (ctx->vec_fixed == 4 && !life_torus(ctx)) G = std::min<int64_t>(G, kMaxGensVec4Generic);
+    // 16-byte lanes (forced by tuning, or implied by the quad layout): the
+    // generic-rule / clipped instances deeper than this spill (gol_set_tuning
+    // refuses them as fixed depths with words_per_lane = 4)
+    if ((ctx->vec_fixed == 4 || ctx->ilv == 4) && !life_torus(ctx))
+        G = std::min<int64_t>(G, kMaxGensVec4Generic);
     if (in_ring(ctx)) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return (int)std::max<int64_t>(G, 1);
@@ -1257,6 +1290,13 @@ int gol_shard_rows(int64_t height, int rank, int nranks, int64_t* row0, int64_t*
     return GOL_OK;
 }
 
+int gol_device_layout(int32_t topology, int64_t width, int32_t* words_per_group) {
+    if (!words_per_group || width <= 0 || (topology != GOL_TORUS && topology != GOL_REF_CLIPPED))
+        return set_err(nullptr, GOL_EINVAL, "gol_device_layout: bad arguments");
+    *words_per_group = device_ilv(topology, (width + 31) / 32);
+    return GOL_OK;
+}
+
 int gol_create(gol_ctx** out, const gol_config* cfg) {
     if (!out || !cfg) return set_err(nullptr, GOL_EINVAL, "gol_create: null argument");
     *out = nullptr;
@@ -1313,7 +1353,7 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     ctx->survive = c.survive_mask;
     ctx->vis_w = c.vis_width > 0 ? c.vis_width : c.width - 1;
     ctx->vis_h = c.vis_height > 0 ? c.vis_height : c.height - 1;
-    ctx->pairs = c.topology == GOL_TORUS && wwords % 2 == 0;
+    ctx->ilv = device_ilv(c.topology, wwords);
     ctx->device = c.device;
     ctx->vec_fixed = 0;
     if (hipDeviceGetAttribute(&ctx->num_cus, hipDeviceAttributeMultiprocessorCount, c.device) != hipSuccess) {
@@ -1387,7 +1427,7 @@ int gol_seed(gol_ctx* ctx, uint64_t seed) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (int rc = bind(ctx)) return rc;
     HIP_CHECK(ctx, gol::launch_seed(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->width, ctx->row0,
-                                    (int32_t)ctx->rows, seed, ctx->pairs, ctx->compute));
+                                    (int32_t)ctx->rows, seed, ctx->ilv, ctx->compute));
     ctx->epoch = 0;
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     return GOL_OK;
@@ -1406,13 +1446,13 @@ int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words) {
                 return set_err(ctx, GOL_EINVAL, "padding bits beyond width set in row %lld", (long long)r);
     }
     if (int rc = bind(ctx)) return rc;
-    // pair layout: upload into the spare plane, interleave into the current one
-    uint32_t* dst = ctx->pairs ? ctx->plane[ctx->cur ^ 1] : ctx->plane[ctx->cur];
+    // interleaved layouts: upload into the spare plane, interleave into the current one
+    uint32_t* dst = ctx->ilv > 1 ? ctx->plane[ctx->cur ^ 1] : ctx->plane[ctx->cur];
     HIP_CHECK(ctx, hipMemcpy2DAsync(dst, ctx->pitch * 4, packed, host_pitch_words * 4, (size_t)ctx->wwords * 4,
                                     ctx->rows, hipMemcpyHostToDevice, ctx->compute));
-    if (ctx->pairs)
+    if (ctx->ilv > 1)
         HIP_CHECK(ctx, gol::launch_convert(dst, ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, (int32_t)ctx->rows,
-                                           true, ctx->compute));
+                                           true, ctx->ilv, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     ctx->epoch = 0;
     return GOL_OK;
@@ -1493,7 +1533,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     // they were at the shard's epoch.  Host rows are row-major; a pair-layout
     // board converts them on the device (upload to the other block first).
     const int64_t pitch = ctx->pitch, hp = host_pitch_words;
-    uint32_t* up = ctx->pairs ? blk[1] : blk[0];
+    uint32_t* up = ctx->ilv > 1 ? blk[1] : blk[0];
     auto fail_hip = [&](hipError_t e, const char* what) {
         (void)hipGetLastError();
         release();
@@ -1506,11 +1546,11 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     if (e == hipSuccess)
         e = hipMemcpy2DAsync(up + (n + ctx->rows) * pitch, pitch * 4, below, hp * 4, (size_t)ctx->wwords * 4, n,
                              hipMemcpyHostToDevice, ctx->compute);
-    if (e == hipSuccess && ctx->pairs) {
-        e = gol::launch_convert(up, blk[0], pitch, ctx->wwords, (int32_t)n, true, ctx->compute);
+    if (e == hipSuccess && ctx->ilv > 1) {
+        e = gol::launch_convert(up, blk[0], pitch, ctx->wwords, (int32_t)n, true, ctx->ilv, ctx->compute);
         if (e == hipSuccess)
             e = gol::launch_convert(up + (n + ctx->rows) * pitch, blk[0] + (n + ctx->rows) * pitch, pitch,
-                                    ctx->wwords, (int32_t)n, true, ctx->compute);
+                                    ctx->wwords, (int32_t)n, true, ctx->ilv, ctx->compute);
     }
     if (e == hipSuccess)
         e = hipMemcpyAsync(blk[0] + n * pitch, ctx->plane[ctx->cur], (size_t)ctx->rows * pitch * 4,
@@ -1530,7 +1570,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
         }
         cur ^= 1;
         if (hashes_out) {
-            e = gol::launch_hash(blk[cur] + n * pitch, pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
+            e = gol::launch_hash(blk[cur] + n * pitch, pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows, ctx->ilv,
                                  ctx->slots + (size_t)g * gol::kHashGenStride, ctx->compute);
             if (e != hipSuccess) return fail_hip(e, "light-cone hash");
         }
@@ -1588,7 +1628,7 @@ int gol_hash(gol_ctx* ctx, uint64_t* hash_out) {
     const size_t per = (size_t)gol::kHashSlots * gol::kHashSlotStride;
     HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, per * sizeof(unsigned long long), ctx->compute));
     HIP_CHECK(ctx, gol::launch_hash(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
-                                    ctx->slots, ctx->compute));
+                                    ctx->ilv, ctx->slots, ctx->compute));
     HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, per * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
@@ -1600,12 +1640,12 @@ int gol_snapshot(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_words) {
     if (!ctx || !packed_out) return set_err(ctx, GOL_EINVAL, "null argument");
     if (host_pitch_words < ctx->wwords) return set_err(ctx, GOL_EINVAL, "host pitch too small");
     if (int rc = bind(ctx)) return rc;
-    // pair layout: de-interleave into the spare plane (free between passes:
-    // the compute stream is ordered after every reader of the last pass)
+    // interleaved layouts: de-interleave into the spare plane (free between
+    // passes: the compute stream is ordered after every reader of the last pass)
     const uint32_t* src = ctx->plane[ctx->cur];
-    if (ctx->pairs) {
+    if (ctx->ilv > 1) {
         HIP_CHECK(ctx, gol::launch_convert(src, ctx->plane[ctx->cur ^ 1], ctx->pitch, ctx->wwords,
-                                           (int32_t)ctx->rows, false, ctx->compute));
+                                           (int32_t)ctx->rows, false, ctx->ilv, ctx->compute));
         src = ctx->plane[ctx->cur ^ 1];
     }
     HIP_CHECK(ctx, hipMemcpy2DAsync(packed_out, host_pitch_words * 4, src, ctx->pitch * 4, (size_t)ctx->wwords * 4,
@@ -1640,9 +1680,9 @@ int gol_snapshot_async(gol_ctx* ctx, uint32_t* packed_out, int64_t host_pitch_wo
     if (!ctx->ev_snap_ready) HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_ready, hipEventDisableTiming));
     if (!ctx->ev_snap_done) HIP_CHECK(ctx, hipEventCreateWithFlags(&ctx->ev_snap_done, hipEventDisableTiming));
     const uint32_t* src = ctx->plane[ctx->cur];
-    if (ctx->pairs)
+    if (ctx->ilv > 1)
         HIP_CHECK(ctx, gol::launch_convert(src, ctx->snap, ctx->pitch, ctx->wwords, (int32_t)ctx->rows, false,
-                                           ctx->compute, ctx->wwords));
+                                           ctx->ilv, ctx->compute, ctx->wwords));
     else
         HIP_CHECK(ctx, hipMemcpy2DAsync(ctx->snap, (size_t)ctx->wwords * 4, src, ctx->pitch * 4,
                                         (size_t)ctx->wwords * 4, ctx->rows, hipMemcpyDeviceToDevice, ctx->compute));
@@ -1713,10 +1753,11 @@ int gol_get_cell(gol_ctx* ctx, int64_t x, int64_t y, int* state) {
     if (x < 0 || x >= ctx->width || y < ctx->row0 || y >= ctx->row0 + ctx->rows)
         return set_err(ctx, GOL_EINVAL, "cell (%lld, %lld) not in this shard", (long long)x, (long long)y);
     if (int rc = bind(ctx)) return rc;
-    // row-major: bit x % 32 of word x / 32; pairs: bit (x % 64) / 2 of word
-    // 2 (x / 64) + x % 2
-    const int64_t word = ctx->pairs ? 2 * (x / 64) + (x & 1) : x / 32;
-    const int bit = ctx->pairs ? (int)((x % 64) >> 1) : (int)(x % 32);
+    // row-major: bit x % 32 of word x / 32; interleave groups of k words:
+    // bit (x % 32k) / k of word k (x / 32k) + x % k
+    const int64_t k = ctx->ilv, span = 32 * k;
+    const int64_t word = k * (x / span) + x % k;
+    const int bit = (int)((x % span) / k);
     uint32_t w = 0;
     HIP_CHECK(ctx, hipMemcpyAsync(&w, ctx->plane[ctx->cur] + (y - ctx->row0) * ctx->pitch + word, 4,
                                   hipMemcpyDeviceToHost, ctx->compute));
@@ -1975,7 +2016,7 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int vec = lane_words(ctx, gens_per_pass);
     const int blocks =
-        gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(vec), life, false, clipped, ctx->pairs);
+        gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(ctx, vec, life, gens_per_pass), life, false, clipped, ctx->ilv);
     if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
     if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
     return GOL_OK;

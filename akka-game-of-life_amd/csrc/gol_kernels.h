@@ -19,12 +19,14 @@ constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line ea
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
 constexpr int kMaxGensPerPass = 12;  // temporal blocking depth supported by the kernels
+constexpr int kMaxGensQuadHg = 8;    // deepest horizontal-first pass on the quad layout (2 waves per SIMD)
 
 // State hash keys (DESIGN.md "State hash"; oracle/gol_oracle.c
 // oracle_hash_packed, oracle/oracle.py np_hash): device word w at global row
-// y, device word column c contributes w * A(y, c & 1) * B(c >> 1) mod 2^64.
+// y, device word column c contributes w * A(y, c % HG) * B(c / HG) mod 2^64,
+// HG = 4 on the quad layout, 2 on every other.
 //   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * kHashRowMul (mod 2^32)
-//   A(y, 1) = A(y, 0) + kHashOddAdd        (even: stays odd)
+//   A(y, j) = A(y, 0) + j * kHashOddAdd    (even: stays odd)
 //   B(k)    = murmur3 fmix32(k + kHashPairAdd) | 1
 // Both keys odd, so a single-word change always changes the sum.
 constexpr uint32_t kHashRowMul = 0x9E3779B1u;
@@ -109,27 +111,29 @@ int strip_words(int vec, int gens);
 
 // vec: words per lane (1, 2 or 4); gens: generations per pass; life: B3/S23
 // fast path (torus only); hash: fuse the per-generation state hash; clipped:
-// reference geometry; pairs: the plane is pair-interleaved (even vec only).
-hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, bool pairs,
+// reference geometry; ilv: the plane's interleave (1 row-major, 2 pairs,
+// 4 quads; a multiple of vec).
+hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, int ilv,
                        int grid_x, int grid_y, hipStream_t stream);
 
 // Resident 256-thread workgroups per CU of the step kernel instance a launch
 // with these parameters uses (hipOccupancyMaxActiveBlocksPerMultiprocessor);
 // 0 if unknown.
-int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, bool pairs);
+int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, int ilv);
 
-// Seeded board in the device layout (pairs: pair-interleaved words).
+// Seeded board in the device layout (ilv: words per interleave group).
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width,
-                       int64_t grow0, int32_t rows, uint64_t seed, bool pairs, hipStream_t stream);
+                       int64_t grow0, int32_t rows, uint64_t seed, int ilv, hipStream_t stream);
 
-// Row-major words <-> pair-interleaved words, `rows` rows of `wwords` (even)
-// words, `pitch` words apart in the source and `dst_pitch` (<= 0: `pitch`)
-// in the destination (src != dst).
+// Row-major words <-> interleaved words (ilv 2: pairs, 4: quads), `rows` rows
+// of `wwords` (a multiple of ilv) words, `pitch` words apart in the source
+// and `dst_pitch` (<= 0: `pitch`) in the destination (src != dst).
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
-                          bool to_pairs, hipStream_t stream, int64_t dst_pitch = 0);
+                          bool to_device, int ilv, hipStream_t stream, int64_t dst_pitch = 0);
 
+// Partial state hash of `rows` device rows (hash group 4 on the quad layout).
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0,
-                       int32_t rows, unsigned long long* slots, hipStream_t stream);
+                       int32_t rows, int ilv, unsigned long long* slots, hipStream_t stream);
 
 // DPP / lane-shift self test: out[64*4] (see gol_selftest in gol_capi.cpp).
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream);

@@ -50,8 +50,14 @@ constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
 #ifndef GOL_HG_PF
 #define GOL_HG_PF 2
 #endif
-constexpr int kHgPF = GOL_HG_PF;     // multistep_hg_kernel: rows prefetched ahead (< kMRing)
-static_assert(kHgPF >= 1 && kHgPF < kMRing, "prefetch slots");
+#ifndef GOL_HG_PF_QUAD
+#define GOL_HG_PF_QUAD 2
+#endif
+// multistep_hg_kernel: rows prefetched ahead (< kMRing); 16-byte (quad) lanes
+// run at 2 waves per SIMD and may prefetch deeper
+template <int VEC>
+constexpr int kHgPF = VEC == 4 ? GOL_HG_PF_QUAD : GOL_HG_PF;
+static_assert(kHgPF<2> >= 1 && kHgPF<2> < kMRing && kHgPF<4> >= 1 && kHgPF<4> < kMRing, "prefetch slots");
 #ifndef GOL_IDLE_LANES_OFF
 #define GOL_IDLE_LANES_OFF 1        // multistep_hg_kernel: lanes past the last strip's halo lane exit
 #endif
@@ -333,41 +339,43 @@ __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC
 // (pp ^ c0 = 1 means exactly one of pp, c0 is set, so bit 2 is qq; n = 8 has
 // pp = c0 = 0 and dies) -- two v_bitop3 after the adder.
 //
-// PAIRS (pair-interleaved words, DESIGN.md "Data layout"): word j even holds
-// the even columns of a 64-column pair, word j+1 the odd ones, so column x-1
-// of an even-column word is the odd word shifted up one bit (the bit shifted
-// in is the previous pair's last odd column) and column x+1 is the odd word
-// itself; mirror-wise for odd-column words.  One funnel shift per word
-// instead of two (v_alignbit issues at half the rate of v_bitop3 on gfx950).
-template <int VEC, bool LIFE, bool PAIRS, bool CLIPPED>
+// ILV (interleaved words, DESIGN.md "Data layout"): a group of ILV words
+// holds 32 * ILV consecutive columns, column 32 ILV k + ILV b + j in bit b of
+// word j of group k.  The column left of word j > 0 is word j - 1 itself and
+// the column right of word j < ILV - 1 is word j + 1 itself; only word 0's west
+// neighbour (the group's last word shifted up one bit, the bit shifted in
+// being the previous group's last column) and the last word's east neighbour
+// (the group's first word shifted down, the next group's first column coming
+// in) need a funnel shift.  ILV = 1 is the row-major layout (two shifts per
+// word), ILV = 2 the pair layout (one per word), ILV = 4 the quad layout (one
+// per two words) -- v_alignbit issues at half the rate of v_bitop3 on gfx950.
+template <int ILV, int VEC, typename T>
+__device__ __forceinline__ void neighbours(const T (&v)[VEC], T l, T r, int j, T& w, T& e) {
+    // l: the word left of word 0 (the previous lane's last), r: the word right
+    // of word VEC - 1 (the next lane's first)
+    const T lw = j == 0 ? l : v[j - 1];
+    const T re = j == VEC - 1 ? r : v[j + 1];
+    if constexpr (ILV == 1) {
+        w = __builtin_amdgcn_alignbit(v[j], lw, 31);  // column x-1
+        e = __builtin_amdgcn_alignbit(re, v[j], 1);   // column x+1
+    } else {
+        const int ph = j % ILV;
+        w = ph == 0 ? __builtin_amdgcn_alignbit(v[j + ILV - 1], lw, 31) : lw;
+        e = ph == ILV - 1 ? __builtin_amdgcn_alignbit(re, v[j - ILV + 1], 1) : re;
+    }
+}
+
+template <int VEC, bool LIFE, int ILV, bool CLIPPED>
 __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (&v0)[VEC],
                                            const uint32_t (&v1)[VEC], const uint32_t (&p0)[VEC],
                                            const uint32_t (&p1)[VEC], uint32_t m0, uint32_t m1, uint32_t n0,
                                            uint32_t n1, const Words<VEC>& alive, Words<VEC>& out) {
-    static_assert(!PAIRS || VEC % 2 == 0, "the pair layout needs whole pairs per lane");
+    static_assert(VEC % ILV == 0, "whole interleave groups per lane");
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {
-        const uint32_t l0 = j == 0 ? m0 : v0[j - 1];
-        const uint32_t l1 = j == 0 ? m1 : v1[j - 1];
-        const uint32_t r0 = j == VEC - 1 ? n0 : v0[j + 1];
-        const uint32_t r1 = j == VEC - 1 ? n1 : v1[j + 1];
         uint32_t w0, e0, w1, e1;
-        if (!PAIRS) {
-            w0 = __builtin_amdgcn_alignbit(v0[j], l0, 31);  // column x-1
-            e0 = __builtin_amdgcn_alignbit(r0, v0[j], 1);   // column x+1
-            w1 = __builtin_amdgcn_alignbit(v1[j], l1, 31);
-            e1 = __builtin_amdgcn_alignbit(r1, v1[j], 1);
-        } else if (j % 2 == 0) {  // even columns: r = the pair's odd word, l = previous odd word
-            w0 = __builtin_amdgcn_alignbit(r0, l0, 31);
-            w1 = __builtin_amdgcn_alignbit(r1, l1, 31);
-            e0 = r0;
-            e1 = r1;
-        } else {  // odd columns: l = the pair's even word, r = next even word
-            w0 = l0;
-            w1 = l1;
-            e0 = __builtin_amdgcn_alignbit(r0, l0, 1);
-            e1 = __builtin_amdgcn_alignbit(r1, l1, 1);
-        }
+        neighbours<ILV>(v0, m0, n0, j, w0, e0);
+        neighbours<ILV>(v1, m1, n1, j, w1, e1);
         if constexpr (LIFE && !CLIPPED) {
             // full 9-cell sum S = v(x-1) + v(x) + v(x+1): the gate circuit of
             // rule_hg (rule_b3s23_fullsum); the centre-less pair p is unused
@@ -403,44 +411,55 @@ __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (
 }
 
 // Fused state hash (DESIGN.md "State hash"): device word w at global row y,
-// device word column c contributes w * A(y, c & 1) * B(c >> 1) (mod 2^64).
-// A lane sums w * A over the rows it streams -- one v_mad_u64_u32 per word and
-// generation, the row key A an SGPR computed once per row on the scalar unit
-// -- and multiplies by its column-pair key B once, when it flushes
-// (hash_lane_total).  A lane's words share B: one pair (VEC = 2, the row's
-// first word index even), two pairs (VEC = 4: two sums), or one word of a
+// device word column c contributes w * A(y, c % HG) * B(c / HG) (mod 2^64),
+// HG = 4 on the quad layout and 2 otherwise (kHashGroup), with
+// A(y, j) = A(y, 0) + j kHashOddAdd.  A lane sums w * A over the rows it
+// streams -- one v_mad_u64_u32 per word and generation, the row key A an SGPR
+// computed once per row on the scalar unit -- and multiplies by its column-
+// group key B once, when it flushes (hash_lane_total).  A lane's words share
+// B: one group (VEC = HG, the row's first word index a multiple of HG), two
+// pairs (VEC = 4 on the row-major or pair layouts: two sums), or one word of a
 // pair (VEC = 1: the lane picks the key of its word's parity).
-template <int VEC>
+template <int ILV>
+constexpr int kHashGroup = ILV == 4 ? 4 : 2;
+
+template <int VEC, int HG = 2>
 struct HashAcc {
-    static constexpr int kPairs = VEC >= 2 ? VEC / 2 : 1;
-    unsigned long long a[kPairs];
+    static constexpr int kGroups = VEC >= HG ? VEC / HG : 1;
+    unsigned long long a[kGroups];
 };
 
-template <int VEC>
-__device__ __forceinline__ void hash_clear(HashAcc<VEC>& h) {
+template <int VEC, int HG>
+__device__ __forceinline__ void hash_clear(HashAcc<VEC, HG>& h) {
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k) h.a[k] = 0;
+    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k) h.a[k] = 0;
 }
 
 // One output row with row keys ae = A(y, 0), ao = A(y, 1) (both 0: the row
-// is not hashed); odd_lane: VEC = 1 lanes of odd words.
-template <int VEC>
+// is not hashed; A(y, 2), A(y, 3) follow as 2 ao - ae, 3 ao - 2 ae); odd_lane:
+// VEC = 1 lanes of odd words.
+template <int VEC, int HG>
 __device__ __forceinline__ void hash_row_keys(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
-                                              HashAcc<VEC>& h) {
+                                              HashAcc<VEC, HG>& h) {
     if constexpr (VEC == 1) {
+        static_assert(HG == 2, "a quad spans four words");
         h.a[0] += (unsigned long long)o.w[0] * (unsigned long long)(odd_lane ? ao : ae);
     } else {
+        static_assert(VEC % HG == 0, "whole hash groups per lane");
 #pragma unroll
-        for (int j = 0; j < VEC; ++j)
-            h.a[j / 2] += (unsigned long long)o.w[j] * (unsigned long long)((j & 1) ? ao : ae);
+        for (int j = 0; j < VEC; ++j) {
+            const int ph = j % HG;
+            const uint32_t key = ph == 0 ? ae : ph == 1 ? ao : (uint32_t)ph * ao - (uint32_t)(ph - 1) * ae;
+            h.a[j / HG] += (unsigned long long)o.w[j] * (unsigned long long)key;
+        }
     }
 }
 
 // One output row at global row `grow`.
-template <int VEC>
-__device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool odd_lane, HashAcc<VEC>& h) {
+template <int VEC, int HG>
+__device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool odd_lane, HashAcc<VEC, HG>& h) {
     const uint32_t ae = hash_row_key(grow);
-    hash_row_keys<VEC>(ae, ae + kHashOddAdd, o, odd_lane, h);
+    hash_row_keys<VEC, HG>(ae, ae + kHashOddAdd, o, odd_lane, h);
 }
 
 // The horizontal-first kernel keeps its per-generation sums in LDS, one u64
@@ -449,25 +468,25 @@ __device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool
 #ifndef GOL_HASH_LDS
 #define GOL_HASH_LDS 1
 #endif
-template <int VEC>
+template <int VEC, int HG>
 __device__ __forceinline__ void hash_row_lds(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
                                              unsigned long long* slot) {
-    HashAcc<VEC> t;
+    HashAcc<VEC, HG> t;
     hash_clear(t);
-    hash_row_keys<VEC>(ae, ao, o, odd_lane, t);
+    hash_row_keys<VEC, HG>(ae, ao, o, odd_lane, t);
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k) atomicAdd(slot + k * kWaveLanes, t.a[k]);
+    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k) atomicAdd(slot + k * kWaveLanes, t.a[k]);
 }
 
-// The lane's contribution: its sums times their column-pair keys (words
-// col .. col + VEC - 1; col even when VEC >= 2), or 0 for a lane that owns
-// no words.
-template <int VEC>
-__device__ __forceinline__ unsigned long long hash_lane_total(const HashAcc<VEC>& h, int col, bool owns) {
+// The lane's contribution: its sums times their column-group keys (words
+// col .. col + VEC - 1; col a multiple of HG when VEC >= HG), or 0 for a lane
+// that owns no words.
+template <int VEC, int HG>
+__device__ __forceinline__ unsigned long long hash_lane_total(const HashAcc<VEC, HG>& h, int col, bool owns) {
     unsigned long long t = 0;
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC>::kPairs; ++k)
-        t += h.a[k] * (unsigned long long)hash_pair_key((uint32_t)(col >> 1) + (uint32_t)k);
+    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k)
+        t += h.a[k] * (unsigned long long)hash_pair_key((uint32_t)(col / HG) + (uint32_t)k);
     return owns ? t : 0ull;
 }
 
@@ -503,8 +522,9 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
 #endif
 constexpr bool kG1NtStores = GOL_NT_STORES || GOL_G1_NT_STORES;
 
-template <int VEC, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
+template <int VEC, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
+    constexpr int HG = kHashGroup<ILV>;
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
@@ -513,7 +533,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
     unsigned long long acc = 0;
 
     if (bandi < p.nbands[rg]) {
-        HashAcc<VEC> hacc;
+        HashAcc<VEC, HG> hacc;
         hash_clear(hacc);
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
         const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
@@ -589,7 +609,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
                 n1 = last ? r1 : n1;
             }
             Words<VEC> o;
-            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, RC, o);
+            rule_words<VEC, LIFE, ILV, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, RC, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -597,7 +617,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const int r = out_of(i);
             store_row<VEC, kG1NtStores>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
             if constexpr (HASH) {
-                if (in_band) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc);
+                if (in_band) hash_row<VEC, HG>(p.grow0 + r, o, odd_lane, hacc);
             }
         };
         auto step_i = [&](int i, int u, bool in_band) {
@@ -661,8 +681,9 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
 // --------------------------------------------------------------------------
 // G generations per pass (temporal blocking).
 // --------------------------------------------------------------------------
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(const StepParams p) {
+    constexpr int HG = kHashGroup<ILV>;
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
     constexpr int kOut = (kWaveLanes - 2) * VEC;  // output words per strip
@@ -701,7 +722,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
         }
         const bool odd_lane = (col & 1) != 0;
-        HashAcc<VEC> hacc[G];
+        HashAcc<VEC, HG> hacc[G];
 #pragma unroll
         for (int s = 0; s < G; ++s) hash_clear(hacc[s]);
         const bool up = (bandi & 1) != 0;
@@ -733,7 +754,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             const uint32_t m1 = dpp_shr1_zero(v1[VEC - 1]);
             const uint32_t n0 = dpp_shl1_zero(v0[0]);
             const uint32_t n1 = dpp_shl1_zero(v1[0]);
-            rule_words<VEC, LIFE, PAIRS, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
+            rule_words<VEC, LIFE, ILV, CLIPPED>(p, v0, v1, p0, p1, m0, m1, n0, n1, C, o);
             if constexpr (CLIPPED) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o.w[j] &= omask[j];
@@ -754,7 +775,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                 if (s < G) {
                     st[s - 1][((u - s) % 3 + 3) % 3] = o;
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p.grow0 + brow(m), o, odd_lane, hacc[s - 1]);
+                        if (own_row) hash_row<VEC, HG>(p.grow0 + brow(m), o, odd_lane, hacc[s - 1]);
                     }
                     // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
                     apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
@@ -763,7 +784,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC>(p.grow0 + r, o, odd_lane, hacc[G - 1]);
+                        if (own_row) hash_row<VEC, HG>(p.grow0 + r, o, odd_lane, hacc[G - 1]);
                     }
                 }
             }
@@ -807,7 +828,7 @@ struct HRow {
     uint32_t a[CLIPPED ? VEC : 1];       // clipped: the real row (alive bits)
 };
 
-template <int VEC, bool CLIPPED, bool PAIRS>
+template <int VEC, bool CLIPPED, int ILV>
 __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const uint32_t (&cmask)[VEC],
                                        HRow<VEC, CLIPPED>& o) {
     uint32_t rv[VEC];
@@ -818,26 +839,11 @@ __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const ui
     }
     const uint32_t left = dpp_shr1_zero(rv[VEC - 1]);  // halo lanes read zeros at the wave's ends
     const uint32_t right = dpp_shl1_zero(rv[0]);
-    if constexpr (PAIRS) {  // (e, o) pairs: see rule_words
-        static_assert(VEC % 2 == 0 && !CLIPPED, "pair layout");
+    static_assert(ILV == 1 || !CLIPPED, "clipped boards are row-major");
 #pragma unroll
-        for (int j = 0; j < VEC; j += 2) {
-            const uint32_t e = rv[j], od = rv[j + 1];
-            const uint32_t we = __builtin_amdgcn_alignbit(od, j == 0 ? left : rv[j - 1], 31);
-            const uint32_t eo = __builtin_amdgcn_alignbit(j + 2 == VEC ? right : rv[j + 2], e, 1);
-            o.h0[j] = GOL_BITOP3(we, e, od, kXor3);
-            o.h1[j] = GOL_BITOP3(we, e, od, kMaj);
-            o.h0[j + 1] = GOL_BITOP3(e, od, eo, kXor3);
-            o.h1[j + 1] = GOL_BITOP3(e, od, eo, kMaj);
-            o.r[j] = e;
-            o.r[j + 1] = od;
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-        const uint32_t w = __builtin_amdgcn_alignbit(rv[j], j == 0 ? left : rv[j - 1], 31);
-        const uint32_t e = __builtin_amdgcn_alignbit(j == VEC - 1 ? right : rv[j + 1], rv[j], 1);
+    for (int j = 0; j < VEC; ++j) {  // interleaved groups: see rule_words
+        uint32_t w, e;
+        neighbours<ILV>(rv, left, right, j, w, e);
         o.h0[j] = GOL_BITOP3(w, rv[j], e, kXor3);
         o.h1[j] = GOL_BITOP3(w, rv[j], e, kMaj);
         o.r[j] = rv[j];
@@ -897,13 +903,19 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
 #ifndef GOL_HG_MINWAVES_DEEP
 #define GOL_HG_MINWAVES_DEEP 3
 #endif
+// Quad-layout lanes (VEC = 4): two waves per SIMD, 256 VGPRs.
+#ifndef GOL_HG_MINWAVES_QUAD
+#define GOL_HG_MINWAVES_QUAD 2
+#endif
 template <int VEC, int G, bool LIFE, bool HASH>
 constexpr int kHgMinWaves = (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8
-                             : (VEC == 2 && G >= 10 && LIFE && HASH) ? GOL_HG_MINWAVES_DEEP : 1;
+                             : (VEC == 2 && G >= 10 && LIFE && HASH) ? GOL_HG_MINWAVES_DEEP
+                             : (VEC == 4) ? GOL_HG_MINWAVES_QUAD : 1;
 
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH>)) void multistep_hg_kernel(
     const StepParams p) {
+    constexpr int HG = kHashGroup<ILV>;
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
     constexpr int kOut = (kWaveLanes - 2) * VEC;
@@ -915,7 +927,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
     unsigned long long acc[G];
 #pragma unroll
     for (int s = 0; s < G; ++s) acc[s] = 0;
-    __shared__ unsigned long long hash_lds[HASH ? kWavesPerWG * G * HashAcc<VEC>::kPairs * kWaveLanes : 1];
+    __shared__ unsigned long long hash_lds[HASH ? kWavesPerWG * G * HashAcc<VEC, HG>::kGroups * kWaveLanes : 1];
 
     if (bandi < p.nbands[rg]) {
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
@@ -955,14 +967,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
         }
         const bool odd_lane = (col & 1) != 0;
-        constexpr int kNP = HashAcc<VEC>::kPairs;
+        constexpr int kNP = HashAcc<VEC, HG>::kGroups;
         // this lane's LDS sums: generation s, pair k at hsum[(s * kNP + k) * kWaveLanes]
         unsigned long long* hsum = hash_lds + (size_t)wave_in_wg * G * kNP * kWaveLanes + lane;
         if constexpr (HASH) {
 #pragma unroll
             for (int k = 0; k < G * kNP; ++k) hsum[k * kWaveLanes] = 0ull;
         }
-        HashAcc<VEC> hreg[GOL_HASH_LDS ? 1 : G];  // -DGOL_HASH_LDS=0: register sums (A/B builds)
+        HashAcc<VEC, HG> hreg[GOL_HASH_LDS ? 1 : G];  // -DGOL_HASH_LDS=0: register sums (A/B builds)
 #pragma unroll
         for (int s = 0; s < (GOL_HASH_LDS ? 1 : G); ++s) hash_clear(hreg[s]);
         const bool up = (bandi & 1) != 0;
@@ -995,14 +1007,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 #pragma unroll
         for (int k = 0; k <= G; ++k) kae[k] = kao[k] = 0u;
 
-        // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF,
+        // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF<VEC>,
         // input row q arrives at ring 0, stage s produces stream row q - s.
         // Stage s has valid inputs only from q = 2s on (its rows m < s are
         // built from the clamped rows before the band and are never stored,
         // hashed or read by a valid row), so the pipeline fill -- the first
         // kFill rows, q known at compile time -- skips those stage steps.
         auto row_step = [&](const int q, const int u, const bool fill) __attribute__((always_inline)) {
-            load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
+            load_m(min(q + kHgPF<VEC>, n_in - 1), in[(u + kHgPF<VEC>) % kMRing]);
             if constexpr (HASH) {
 #pragma unroll
                 for (int k = G; k >= 1; --k) {
@@ -1014,7 +1026,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
                 kae[0] = own_q ? ae : 0u;
                 kao[0] = own_q ? ae + kHashOddAdd : 0u;
             }
-            arrive<VEC, CLIPPED, PAIRS>(in[u], vis(q), cmask, hr[0][u % 3]);
+            arrive<VEC, CLIPPED, ILV>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
             for (int s = 1; s <= G; ++s) {
                 if (fill && q < 2 * s) break;  // stages s.. have no valid row yet
@@ -1027,13 +1039,13 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
                 const bool own_row = m >= G && m < n_in - G;
                 if constexpr (HASH) {
 #if GOL_HASH_LDS
-                    hash_row_lds<VEC>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
+                    hash_row_lds<VEC, HG>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
 #else
-                    hash_row_keys<VEC>(kae[s], kao[s], o, odd_lane, hreg[s - 1]);
+                    hash_row_keys<VEC, HG>(kae[s], kao[s], o, odd_lane, hreg[s - 1]);
 #endif
                 }
                 if (s < G) {
-                    arrive<VEC, CLIPPED, PAIRS>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
+                    arrive<VEC, CLIPPED, ILV>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
                 } else {
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
@@ -1042,7 +1054,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         };
 
 #pragma unroll
-        for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
+        for (int t = 0; t < kHgPF<VEC>; ++t) load_m(min(t, n_in - 1), in[t]);
 #ifndef GOL_HASH_PEEL_MAXG
 #define GOL_HASH_PEEL_MAXG 12
 #endif
@@ -1065,7 +1077,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         if constexpr (HASH) {
 #pragma unroll
             for (int s = 0; s < G; ++s) {
-                HashAcc<VEC> h;
+                HashAcc<VEC, HG> h;
 #pragma unroll
                 for (int k = 0; k < kNP; ++k) {
                     if constexpr (GOL_HASH_LDS) h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
@@ -1084,26 +1096,28 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 
 // The horizontal-first kernel keeps three planes per ring row: at 16-byte
 // lanes it needs 183-270 registers or spills (1-1.6 KB scratch per lane), so
-// VEC = 4 always runs the vertical-first kernel (kernel_variant()).
-template <int VEC>
-constexpr bool kHgLanes = VEC <= 2;
+// VEC = 4 runs the vertical-first kernel (kernel_variant()) -- except the
+// B3/S23 quad layout, whose full-sum circuit needs fewer planes and whose
+// interleave halves the shifts: 2 waves per SIMD (kHgMinWaves).
+template <int VEC, int ILV, bool LIFE, int G>
+constexpr bool kHgLanes = VEC <= 2 || (ILV == 4 && LIFE && G <= kMaxGensQuadHg);
 
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     const dim3 grid(gx, gy), block(kWaveLanes * kWavesPerWG);
     if constexpr (G == 1) {
-        return launch_kernel(step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
+        return launch_kernel(step_kernel<VEC, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     } else {
-        if constexpr (kHgLanes<VEC>) {
+        if constexpr (kHgLanes<VEC, ILV, LIFE, G>) {
             if (p.variant == 2)
-                return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
+                return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
         }
-        return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>, grid, block, st, p);
+        return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     }
 }
 
 // Resident 256-thread workgroups per CU for a kernel instance (occupancy API).
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, bool PAIRS>
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 int blocks_one(int variant) {
     auto query = [](auto kernel) {
         int n = 0;
@@ -1114,69 +1128,78 @@ int blocks_one(int variant) {
         return n;
     };
     if constexpr (G == 1) {
-        return query(step_kernel<VEC, LIFE, HASH, CLIPPED, PAIRS>);
+        return query(step_kernel<VEC, LIFE, HASH, CLIPPED, ILV>);
     } else {
-        if constexpr (kHgLanes<VEC>) {
-            if (variant == 2) return query(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>);
+        if constexpr (kHgLanes<VEC, ILV, LIFE, G>) {
+            if (variant == 2) return query(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>);
         }
-        return query(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, PAIRS>);
+        return query(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>);
     }
 }
 
 // The instances a launch can select: clipped boards (generic rule, row-major
-// words), tori (B3/S23 fast path or generic rule) in row-major or pair layout
-// (even lane widths only).  `F` is called with the instance's template
-// arguments as std::integral_constant values.
+// words), tori (B3/S23 fast path or generic rule) in row-major, pair (even
+// lane widths) or quad layout (4-word lanes).  `F` is called with the
+// instance's template arguments as std::integral_constant values.
 template <int VEC, typename F>
-auto dispatch_kind(bool life, bool hash, bool clipped, bool pairs, F&& f) {
+auto dispatch_kind(bool life, bool hash, bool clipped, int ilv, F&& f) {
     using T = std::true_type;
     using N = std::false_type;
-    if (clipped) return hash ? f(N{}, T{}, T{}, N{}) : f(N{}, N{}, T{}, N{});
-    if (pairs) {
-        if constexpr (VEC % 2 == 0) {
-            if (life) return hash ? f(T{}, T{}, N{}, T{}) : f(T{}, N{}, N{}, T{});
-            return hash ? f(N{}, T{}, N{}, T{}) : f(N{}, N{}, N{}, T{});
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+    if (clipped) return hash ? f(N{}, T{}, T{}, I1{}) : f(N{}, N{}, T{}, I1{});
+    if constexpr (VEC % 4 == 0) {
+        if (ilv == 4) {
+            if (life) return hash ? f(T{}, T{}, N{}, I4{}) : f(T{}, N{}, N{}, I4{});
+            return hash ? f(N{}, T{}, N{}, I4{}) : f(N{}, N{}, N{}, I4{});
         }
     }
-    if (life) return hash ? f(T{}, T{}, N{}, N{}) : f(T{}, N{}, N{}, N{});
-    return hash ? f(N{}, T{}, N{}, N{}) : f(N{}, N{}, N{}, N{});
+    if constexpr (VEC % 2 == 0) {
+        if (ilv == 2) {
+            if (life) return hash ? f(T{}, T{}, N{}, I2{}) : f(T{}, N{}, N{}, I2{});
+            return hash ? f(N{}, T{}, N{}, I2{}) : f(N{}, N{}, N{}, I2{});
+        }
+    }
+    if (life) return hash ? f(T{}, T{}, N{}, I1{}) : f(T{}, N{}, N{}, I1{});
+    return hash ? f(N{}, T{}, N{}, I1{}) : f(N{}, N{}, N{}, I1{});
 }
 
 template <int VEC, int G>
-int blocks_variant(int variant, bool life, bool hash, bool clipped, bool pairs) {
-    if (pairs && VEC % 2 != 0) return 0;
-    return dispatch_kind<VEC>(life, hash, clipped, pairs, [&](auto L, auto H, auto C, auto P) {
-        return blocks_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(P)::value>(
+int blocks_variant(int variant, bool life, bool hash, bool clipped, int ilv) {
+    if (VEC % ilv != 0) return 0;
+    return dispatch_kind<VEC>(life, hash, clipped, ilv, [&](auto L, auto H, auto C, auto I) {
+        return blocks_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(I)::value>(
             variant);
     });
 }
 
 template <int G>
-int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped, bool pairs) {
+int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped, int ilv) {
     switch (vec) {
-        case 4: return blocks_variant<4, G>(variant, life, hash, clipped, pairs);
-        case 2: return blocks_variant<2, G>(variant, life, hash, clipped, pairs);
-        default: return blocks_variant<1, G>(variant, life, hash, clipped, pairs);
+        case 4: return blocks_variant<4, G>(variant, life, hash, clipped, ilv);
+        case 2: return blocks_variant<2, G>(variant, life, hash, clipped, ilv);
+        default: return blocks_variant<1, G>(variant, life, hash, clipped, ilv);
     }
 }
 
 template <int VEC, int G>
-hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, bool pairs, int gx, int gy,
+hipError_t launch_variant(const StepParams& p, bool life, bool hash, bool clipped, int ilv, int gx, int gy,
                           hipStream_t st) {
-    if (pairs && VEC % 2 != 0) return hipErrorInvalidValue;  // checked by the host layer
-    return dispatch_kind<VEC>(life, hash, clipped, pairs, [&](auto L, auto H, auto C, auto P) {
-        return launch_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(P)::value>(
+    if (VEC % ilv != 0) return hipErrorInvalidValue;  // checked by the host layer
+    return dispatch_kind<VEC>(life, hash, clipped, ilv, [&](auto L, auto H, auto C, auto I) {
+        return launch_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(I)::value>(
             p, gx, gy, st);
     });
 }
 
 template <int G>
-hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool clipped, bool pairs, int gx, int gy,
+hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool clipped, int ilv, int gx, int gy,
                        hipStream_t st) {
     switch (vec) {
-        case 4: return launch_variant<4, G>(p, life, hash, clipped, pairs, gx, gy, st);
-        case 2: return launch_variant<2, G>(p, life, hash, clipped, pairs, gx, gy, st);
-        case 1: return launch_variant<1, G>(p, life, hash, clipped, pairs, gx, gy, st);
+        case 4: return launch_variant<4, G>(p, life, hash, clipped, ilv, gx, gy, st);
+        case 2: return launch_variant<2, G>(p, life, hash, clipped, ilv, gx, gy, st);
+        case 1: return launch_variant<1, G>(p, life, hash, clipped, ilv, gx, gy, st);
         default: return hipErrorInvalidValue;
     }
 }
@@ -1184,29 +1207,29 @@ hipError_t launch_gens(const StepParams& p, int vec, bool life, bool hash, bool 
 }  // namespace dev
 
 // Defined one per translation unit (gol_step_g<G>.hip).
-hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g9(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g10(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g11(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-hipError_t launch_step_g12(const StepParams&, int, bool, bool, bool, bool, int, int, hipStream_t);
-int blocks_step_g1(int, int, bool, bool, bool, bool);
-int blocks_step_g2(int, int, bool, bool, bool, bool);
-int blocks_step_g3(int, int, bool, bool, bool, bool);
-int blocks_step_g4(int, int, bool, bool, bool, bool);
-int blocks_step_g5(int, int, bool, bool, bool, bool);
-int blocks_step_g6(int, int, bool, bool, bool, bool);
-int blocks_step_g7(int, int, bool, bool, bool, bool);
-int blocks_step_g8(int, int, bool, bool, bool, bool);
-int blocks_step_g9(int, int, bool, bool, bool, bool);
-int blocks_step_g10(int, int, bool, bool, bool, bool);
-int blocks_step_g11(int, int, bool, bool, bool, bool);
-int blocks_step_g12(int, int, bool, bool, bool, bool);
+hipError_t launch_step_g1(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g2(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g3(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g4(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g5(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g6(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g7(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g8(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g9(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g10(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g11(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+hipError_t launch_step_g12(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
+int blocks_step_g1(int, int, bool, bool, bool, int);
+int blocks_step_g2(int, int, bool, bool, bool, int);
+int blocks_step_g3(int, int, bool, bool, bool, int);
+int blocks_step_g4(int, int, bool, bool, bool, int);
+int blocks_step_g5(int, int, bool, bool, bool, int);
+int blocks_step_g6(int, int, bool, bool, bool, int);
+int blocks_step_g7(int, int, bool, bool, bool, int);
+int blocks_step_g8(int, int, bool, bool, bool, int);
+int blocks_step_g9(int, int, bool, bool, bool, int);
+int blocks_step_g10(int, int, bool, bool, bool, int);
+int blocks_step_g11(int, int, bool, bool, bool, int);
+int blocks_step_g12(int, int, bool, bool, bool, int);
 
 }  // namespace gol

@@ -4,13 +4,13 @@
 
 namespace gol {
 
-hipError_t launch_step_g3(const StepParams& p, int vec, bool life, bool hash, bool clipped, bool pairs, int gx,
+hipError_t launch_step_g3(const StepParams& p, int vec, bool life, bool hash, bool clipped, int ilv, int gx,
                           int gy, hipStream_t st) {
-    return dev::launch_gens<3>(p, vec, life, hash, clipped, pairs, gx, gy, st);
+    return dev::launch_gens<3>(p, vec, life, hash, clipped, ilv, gx, gy, st);
 }
 
-int blocks_step_g3(int vec, int variant, bool life, bool hash, bool clipped, bool pairs) {
-    return dev::blocks_gens<3>(vec, variant, life, hash, clipped, pairs);
+int blocks_step_g3(int vec, int variant, bool life, bool hash, bool clipped, int ilv) {
+    return dev::blocks_gens<3>(vec, variant, life, hash, clipped, ilv);
 }
 
 }  // namespace gol

@@ -139,6 +139,7 @@ _SIGNATURES = {
     "gol_diag_absorbed": (_c.c_int, [_u64p, _c.c_char_p, _c.c_size_t]),
     "gol_profile_stats_read": (_c.c_int, [_vp, ctypes.POINTER(GolProfileStats)]),
     "gol_runtime_info_get": (_c.c_int, [ctypes.POINTER(GolRuntimeInfo)]),
+    "gol_device_layout": (_c.c_int, [_c.c_int32, _c.c_int64, ctypes.POINTER(_c.c_int32)]),
 }
 
 
@@ -180,11 +181,30 @@ def device_count() -> int:
     return n.value
 
 
+def device_ilv(width: int, topology: int = GOL_TORUS) -> int:
+    """Words per interleave group of libgol's device layout (gol_capi.cpp
+    device_ilv): a torus whose rows hold whole pairs of 32-bit words is
+    pair-interleaved (2) -- quad-interleaved (4) when they hold whole quads
+    and GOL_LAYOUT=quads (the opt-in layout) -- any other board row-major (1);
+    the state hash is defined over those device words."""
+    ww = (width + 31) // 32
+    if topology != GOL_TORUS:
+        return 1
+    if ww % 4 == 0 and os.environ.get("GOL_LAYOUT") == "quads":
+        return 4
+    return 2 if ww % 2 == 0 else 1
+
+
 def pair_layout(width: int, topology: int = GOL_TORUS) -> bool:
-    """True when libgol keeps the board pair-interleaved in HBM (gol_capi.cpp
-    gol_create: a torus with an even number of 32-bit words per row); the
-    state hash is defined over those device words."""
-    return topology == GOL_TORUS and ((width + 31) // 32) % 2 == 0
+    """True when libgol keeps the board pair-interleaved in HBM."""
+    return device_ilv(width, topology) == 2
+
+
+def device_layout(width: int, topology: int = GOL_TORUS) -> int:
+    """libgol's own answer (gol_device_layout) -- device_ilv restates it."""
+    k = ctypes.c_int32(0)
+    check(lib.gol_device_layout(topology, width, ctypes.byref(k)))
+    return k.value
 
 
 def shard_rows(height: int, rank: int, nranks: int) -> tuple[int, int]:

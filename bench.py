@@ -67,8 +67,12 @@ DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass
 # 6-row unroll = 648 bitop3 + 72 alignbit + 72 DPP + loop overhead) and the
 # measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
 VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
+# The quad layout (4 interleaved words per lane): one
+# funnel shift and one DPP move per quad edge, i.e. half of each per word.
+VALU_MIX_QUAD = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (0.5, 4.1), "v_mov_b32_dpp": (0.5, 4.3)}
 # The fused hash adds one v_mad_u64_u32 per word and generation (DESIGN.md "State hash").
 VALU_MIX_HASH = dict(VALU_MIX, v_mad_u64_u32=(1, 4.6))
+VALU_MIX_QUAD_HASH = dict(VALU_MIX_QUAD, v_mad_u64_u32=(1, 4.6))
 
 
 def parse():
@@ -95,9 +99,10 @@ class Job:
     Ranks come from the launcher's environment (torch.distributed.run sets
     RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Rank 0's RCCL
     unique id reaches the other ranks through a file named after
-    MASTER_ADDR:MASTER_PORT and the launcher's pid (every local rank is its
-    child; one node); after the first barrier over the new communicator
-    every rank has read it, and rank 0 removes it.  Barriers and the
+    MASTER_ADDR:MASTER_PORT (one node); a file older than this rank's start
+    (minus two minutes of launch skew) is a leftover of an earlier job and is
+    ignored.  After the first barrier over the new communicator every rank
+    has read it, and rank 0 removes it.  Barriers and the
     max over ranks are gol_comm_allreduce_u64 calls on the shard's own RCCL
     communicator: no torch, no second collective library."""
 
@@ -108,10 +113,11 @@ class Job:
         if self.world != n:
             raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
         self.eng = None  # the engine whose communicator carries the collectives
+        self.t_start = time.time()
 
     def uid_path(self):
         key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
-                        os.environ.get("TORCHELASTIC_RUN_ID", ""), str(os.getppid())])
+                        os.environ.get("TORCHELASTIC_RUN_ID", "")])
         return os.path.join(tempfile.gettempdir(), "gol_bench_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16])
 
     def join(self, eng, N, timeout=300.0):
@@ -127,10 +133,11 @@ class Job:
             t0 = time.monotonic()
             while True:
                 try:
-                    with open(path, "rb") as f:
-                        uid = f.read()
-                    if len(uid) == N.GOL_UNIQUE_ID_BYTES:
-                        break
+                    if os.stat(path).st_mtime >= self.t_start - 120.0:
+                        with open(path, "rb") as f:
+                            uid = f.read()
+                        if len(uid) == N.GOL_UNIQUE_ID_BYTES:
+                            break
                 except OSError:
                     pass
                 if time.monotonic() - t0 > timeout:
@@ -386,10 +393,11 @@ def compact_plan(plan):
     return " + ".join(f"{n} x {g}" for n, g in runs)
 
 
-def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None):
+def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None, quads=False):
     """Roofline of the dominant kernel (see the module docstring).  `clock`:
     GHz the timed launches held, from the in-kernel probe (gol_profile_clock):
-    it prices the held_clock diagnostic, never the primary frac."""
+    it prices the held_clock diagnostic, never the primary frac.  `quads`:
+    the board is quad-interleaved (the loop's mix has half the shifts)."""
     if not launches:
         return None
     avg_s = kms / 1e3 / launches
@@ -409,7 +417,7 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
             r["measured_hbm_frac"] = round(pmc["hbm_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             r["traffic_source"] = "profiles/pmc_launch.json " + ", ".join(pmc["keys"])
         return r
-    mix = VALU_MIX_HASH if hashed else VALU_MIX
+    mix = (VALU_MIX_QUAD_HASH if hashed else VALU_MIX_QUAD) if quads else (VALU_MIX_HASH if hashed else VALU_MIX)
     # frac: against the VALU-issue ceiling at the guide's max clock (2.4 GHz,
     # MI355X_MICROARCH.md) -- the peak the chip is specified for.  The clock
     # these launches actually held (in-kernel probe, gol_profile_clock) only
@@ -445,20 +453,28 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
     return r
 
 
-def kernel_label(info, depths):
+def quad_hg(ilv, plan):
+    """Do the plan's passes run the quad-layout horizontal-first kernel (half
+    the shifts: VALU_MIX_QUAD)?  Quads up to 8 generations per pass do."""
+    return ilv == 4 and bool(plan) and max(plan) <= 8
+
+
+def kernel_label(info, depths, ilv=2):
     """Name of the kernel instances the timed passes launch (depths: the pass
     plan, gol_pass_plan): the strip width (gol_occupancy) gives the words per
-    lane; multi-generation passes at 8-byte lanes or narrower run the
-    horizontal-first kernel (gol_capi.cpp kernel_variant)."""
+    lane; multi-generation passes at 8-byte lanes or narrower, and on the quad
+    layout up to 8 generations, run the horizontal-first kernel (gol_capi.cpp
+    kernel_variant); ilv = the board's interleave (gol_device_layout)."""
     gs = sorted(set(depths)) or [1]
     waves, strip = info.get(gs[-1], (0, 0))
+    lay = {1: "row-major", 2: "pairs", 4: "quads"}.get(ilv, ilv)
     if gs == [1]:
         vec = strip // 64 if strip else "VEC"
-        return f"gol::dev::step_kernel<{vec},LIFE>"
+        return f"gol::dev::step_kernel<{vec},LIFE,{lay}>"
     vec = strip // 62 if strip else 0
-    name = "multistep_hg_kernel" if vec in (1, 2) and os.environ.get("GOL_STENCIL_VARIANT", "2") != "1" \
-        else "multistep_kernel"
-    return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE> ({waves} waves/CU resident)"
+    hg = os.environ.get("GOL_STENCIL_VARIANT", "2") != "1" and (vec in (1, 2) or (ilv == 4 and gs[-1] <= 8))
+    name = "multistep_hg_kernel" if hg else "multistep_kernel"
+    return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE,{lay}> ({waves} waves/CU resident)"
 
 
 def settle(eng, ms, chunk, job=None):
@@ -520,7 +536,8 @@ def secondary_run(GolEngine, a, local, parity=None):
         dt1, kms1, l1, g1, c1, _ = fresh_window(e2, None, n1, 0, a.hash, 50.0, 16)
         p1 = chk("65536^2 single-generation passes: gol_hash after K", shape, n1, e2.hash())
     sh = f"{S}x{S}"
-    r2 = roofline(kms2, l2, g2, S * S, plan2, sh, "N1", a.hash, c2)
+    ilv = N_layout(S)
+    r2 = roofline(kms2, l2, g2, S * S, plan2, sh, "N1", a.hash, c2, quad_hg(ilv, plan2))
     r1 = roofline(kms1, l1, g1, S * S, [1] * n1, sh, "N1", a.hash, c1)
     out.update({
         "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2,
@@ -596,8 +613,15 @@ def ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity):
         "unit": "GCUPS", "warmup": f"{a.warmup} ({warm}, after 1 s idle)", "ms_per_step": round(dt8 / a.steps * 1e3, 4),
         "pass_plan": plan8, "exchange": ring_stats(st8, l8), "parity": p8,
         "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
-                                    f"{W}x{rows8}", "ring", False, c8)}
+                                    f"{W}x{rows8}", "ring", False, c8, quad_hg(N_layout(W), plan8))}
     return out
+
+
+def N_layout(width):
+    """Words per interleave group of a torus of `width` columns
+    (gol_device_layout)."""
+    from gameoflife import _native as N
+    return N.device_layout(width)
 
 
 def lib_fingerprint(info):
@@ -632,6 +656,7 @@ def main():
     from gameoflife.engine import GolEngine
     rank, world, local = job.rank, job.world, job.local
     info = N.runtime_info()
+    ilv = N_layout(a.board)
 
     W = H = a.board
     parity = Parity()
@@ -685,17 +710,18 @@ def main():
         hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
                   "frac_of_unhashed": round(vh / value, 4), "pass_plan": hplan,
                   "roofline": roofline(kmsh, lh, gh, W * rows if world == 1 else W * max(rows - round(2 * gh / max(lh, 1)), 0),
-                                       hplan, f"{W}x{rows}", "N1" if world == 1 else "ring", True, ch)}
+                                       hplan, f"{W}x{rows}", "N1" if world == 1 else "ring", True, ch,
+                                       quad_hg(ilv, hplan))}
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
     G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
     if world == 1:
-        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash, clk)
+        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash, clk, quad_hg(ilv, plan))
     else:
         roof = roofline(kms, launches, gcov, W * max(rows - round(2 * G), 0), plan, f"{W}x{rows}", "ring", a.hash,
-                        clk)
+                        clk, quad_hg(ilv, plan))
     if roof is not None:
-        roof["kernel"] = kernel_label(eng_info, plan)
+        roof["kernel"] = kernel_label(eng_info, plan, ilv)
     ring = None
     if world == 1 and not a.no_ring and not a.hash:
         ring = ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity)
@@ -725,6 +751,7 @@ def main():
                                    f"row-block x{world}, G-deep RCCL halo send/recv per pass (ring over xGMI)"),
                    "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash),
+                   "layout": {1: "row-major", 2: "pairs", 4: "quads"}.get(ilv, ilv),
                    "window": "seed, 100 ms untimed settle, re-seed, W warm-up + K timed generations"},
         "roofline": roof,
         "parity": parity.report(),

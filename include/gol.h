@@ -22,12 +22,12 @@
  * Host buffers (gol_load, gol_snapshot, checkpoints): bit-packed rows,
  * row = y, bit (x % 32) of 32-bit word (x / 32) is cell x (LSB first); words
  * per row = ceil(width / 32); bits at x >= width are zero.
- * Device layout (internal): the same rows, except that a torus with an even
- * number of words per row is kept pair-interleaved -- word 2k holds the even
- * columns of columns 64k..64k+63 (bit b = column 64k + 2b), word 2k+1 the odd
- * ones.  The state hash is defined over these device words (DESIGN.md
- * "State hash").  Two device planes (current / next) are swapped after every
- * pass.
+ * Device layout (internal): the same rows, except that tori are kept
+ * interleaved (gol_device_layout): quads when a row holds a multiple of 4
+ * words -- word 4k + j holds columns 128k + 4b + j (bit b) -- else pairs when
+ * it holds an even number -- word 2k + j holds columns 64k + 2b + j.  The
+ * state hash is defined over these device words (DESIGN.md "State hash").
+ * Two device planes (current / next) are swapped after every pass.
  */
 #ifndef GOL_H
 #define GOL_H
@@ -115,6 +115,14 @@ int gol_device_count(int* count);
  * of n owns rows [row0, row0 + rows) of a board `height` rows tall.  Pure
  * host arithmetic.  Replaces the random placement of BoardCreator.scala:33-36. */
 int gol_shard_rows(int64_t height, int rank, int nranks, int64_t* row0, int64_t* rows);
+
+/* Device layout of a board (pure host arithmetic):
+ * *words_per_group = 4 when a torus row holds whole quads of 32-bit words
+ * (column 128g + 4b + j in bit b of word 4g + j), 2 when it holds whole
+ * pairs (column 64g + 2b + j in bit b of word 2g + j), 1 (row-major: column
+ * x in bit x % 32 of word x / 32) otherwise and on clipped boards.  The state
+ * hash is defined over these device words (gol_hash, gol_step's hashes). */
+int gol_device_layout(int32_t topology, int64_t width, int32_t* words_per_group);
 
 /* Seed the shard with the counter-based splitmix64 board (Bernoulli(0.5)),
  * identical for any sharding; resets the epoch to 0.  Seeded stand-in for

@@ -70,6 +70,9 @@ def lib():
         L.oracle_hash_packed.restype = ctypes.c_uint64
         L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64, ctypes.c_int]
         L.oracle_pair_layout.argtypes = [ctypes.c_int, _i64]
+        L.oracle_device_ilv.argtypes = [ctypes.c_int, _i64]
+        L.oracle_quad_word.restype = ctypes.c_uint32
+        L.oracle_quad_word.argtypes = [_u32p, ctypes.c_int]
         L.oracle_hash_row_key.restype = ctypes.c_uint32
         L.oracle_hash_row_key.argtypes = [_i64, ctypes.c_int]
         L.oracle_hash_pair_key.restype = ctypes.c_uint32
@@ -165,47 +168,66 @@ def run_packed(packed: np.ndarray, W: int, gens: int, topology: int = TORUS, rul
     return board, hashes
 
 
+def device_ilv(W: int, topology: int = TORUS) -> int:
+    """Words per interleave group of the engine's device layout (gol_oracle.c
+    oracle_device_ilv): 2 (pairs) for a torus whose rows hold an even number
+    of words -- 4 (quads) for one holding a multiple of 4 with GOL_LAYOUT=quads
+    -- 1 (row-major) else."""
+    return int(lib().oracle_device_ilv(topology, wwords(W)))
+
+
 def pair_layout(W: int, topology: int = TORUS) -> bool:
-    """True when the engine stores the board pair-interleaved (gol_oracle.c
-    oracle_pair_layout): a torus with an even number of words per row."""
-    return bool(lib().oracle_pair_layout(topology, wwords(W)))
+    """True when the engine stores the board pair-interleaved."""
+    return device_ilv(W, topology) == 2
 
 
 def hash_packed(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
     """State hash of row-major packed rows [row0, row0 + rows) of a board
-    (over its device words: pair-interleaved for even-width tori)."""
+    (over its device words: interleaved for tori, oracle_device_ilv)."""
     packed = np.ascontiguousarray(packed, dtype=np.uint32)
     rows, pitch = packed.shape
     return int(lib().oracle_hash_packed(_p(packed, _u32p), wwords(W), row0, rows, pitch,
-                                        int(pair_layout(W, topology))))
+                                        device_ilv(W, topology)))
 
 
 # ------------------------------------------------- independent numpy restatement
 
+def np_ilv(W: int, topology: int = TORUS) -> int:
+    """numpy-side restatement of the layout rule: tori interleave groups of 2
+    words when a row holds whole pairs (4 when it holds whole quads and
+    GOL_LAYOUT=quads)."""
+    ww = wwords(W)
+    if topology != TORUS:
+        return 1
+    if ww % 4 == 0 and os.environ.get("GOL_LAYOUT") == "quads":
+        return 4
+    return 2 if ww % 2 == 0 else 1
+
+
 def np_device_words(packed: np.ndarray, W: int, topology: int = TORUS) -> np.ndarray:
     """Row-major packed rows -> the engine's device words (independent numpy
-    restatement of the layout rule: an even-width torus is pair-interleaved,
-    column 64k + 2b -> bit b of word 2k, column 64k + 2b + 1 -> bit b of
-    word 2k + 1)."""
+    restatement of the layout: with k words per group, column 32 k g + k b + j
+    -> bit b of word k g + j)."""
     ww = wwords(W)
     p = np.asarray(packed, dtype=np.uint32)[:, :ww]
-    if not (topology == TORUS and ww % 2 == 0):
+    k = np_ilv(W, topology)
+    if k == 1:
         return p.copy()
     rows = p.shape[0]
-    bits = ((p[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(rows, ww // 2, 64)
+    bits = ((p[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(rows, ww // k, 32 * k)
     weights = np.uint64(1) << np.arange(32, dtype=np.uint64)
-    even = (bits[:, :, 0::2].astype(np.uint64) * weights).sum(axis=2)
-    odd = (bits[:, :, 1::2].astype(np.uint64) * weights).sum(axis=2)
     out = np.empty((rows, ww), dtype=np.uint32)
-    out[:, 0::2] = even.astype(np.uint32)
-    out[:, 1::2] = odd.astype(np.uint32)
+    for j in range(k):
+        out[:, j::k] = (bits[:, :, j::k].astype(np.uint64) * weights).sum(axis=2).astype(np.uint32)
     return out
 
 
 def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
     """Same hash spec as gol_oracle.c (DESIGN.md "State hash"), written
-    independently with numpy: sum of w * A(y, c & 1) * B(c >> 1) mod 2^64."""
+    independently with numpy: sum of w * A(y, c % G) * B(c / G) mod 2^64,
+    G = 4 on the quad layout, else 2."""
     ww = wwords(W)
+    grp = 4 if np_ilv(W, topology) == 4 else 2
     p = np_device_words(packed, W, topology).astype(np.uint64)
     rows = p.shape[0]
     m32 = np.uint64(0xFFFFFFFF)
@@ -213,8 +235,7 @@ def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) ->
         y = np.arange(rows, dtype=np.uint64) + np.uint64(row0)
         t = (y * np.uint64(0x9E3779B1)) & m32
         a0 = ((((t ^ (t >> np.uint64(15))) << np.uint64(1)) | np.uint64(1)) & m32)
-        a1 = (a0 + np.uint64(0x6A09E666)) & m32
-        k = np.arange(ww, dtype=np.uint64) >> np.uint64(1)
+        k = np.arange(ww, dtype=np.uint64) // np.uint64(grp)
         h = (k + np.uint64(0x7F4A7C15)) & m32
         h ^= h >> np.uint64(16)
         h = (h * np.uint64(0x85EBCA6B)) & m32
@@ -222,8 +243,8 @@ def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) ->
         h = (h * np.uint64(0xC2B2AE35)) & m32
         h ^= h >> np.uint64(16)
         b = h | np.uint64(1)
-        odd = (np.arange(ww) & 1).astype(bool)
-        a = np.where(odd[None, :], a1[:, None], a0[:, None])
+        ph = (np.arange(ww, dtype=np.uint64) % np.uint64(grp))
+        a = (a0[:, None] + ph[None, :] * np.uint64(0x6A09E666)) & m32
         terms = p * (a * b[None, :])
         return int(terms.sum(dtype=np.uint64))
 
