@@ -43,6 +43,7 @@ struct EventPair {
     hipEvent_t start = nullptr, stop = nullptr;
     int clk_slot = -1;  // this launch's clock-probe slot (gol_stencil.h clock_probe_*), or -1
     int kind = kProfMain;
+    int ref = -1;       // exchange / boundary pairs: index of the same pass's interior pair (this fold window)
 };
 
 // Clock-probe slots per context (one per profiled launch between folds).
@@ -115,6 +116,7 @@ struct gol_ctx {
     uint32_t clk_used = 0;                  // slots handed out since the last fold
     double prof_clk_ms_ghz = 0.0, prof_clk_ms = 0.0;  // time-weighted probe clock
     double prof_xchg_ms = 0.0, prof_bnd_ms = 0.0;     // halo exchanges (comm stream), boundary launches (edge)
+    double prof_xchg_exposed_ms = 0.0, prof_tail_ms = 0.0;  // ... how far they end after the interior launch
     uint64_t prof_xchg = 0, prof_bnd = 0;
     uint64_t halo_sent = 0, halo_recv = 0;             // bytes posted to the ring since the last reset
     // occupancy
@@ -283,14 +285,23 @@ int fold_profile(gol_ctx* ctx) {
     }
     for (size_t i = 0; i < ctx->evs_used; ++i) {
         const float ms = times[i];
-        if (ctx->evs[i].kind == kProfExchange) {
+        const int kind = ctx->evs[i].kind, ref = ctx->evs[i].ref;
+        // exposed part: how long after its pass's interior launch this ended
+        float after = 0.f;
+        if ((kind == kProfExchange || kind == kProfBoundary) && ref >= 0 && (size_t)ref < i) {
+            HIP_CHECK(ctx, hipEventElapsedTime(&after, ctx->evs[ref].stop, ctx->evs[i].stop));
+            after = std::max(after, 0.f);
+        }
+        if (kind == kProfExchange) {
             ctx->prof_xchg_ms += ms;
             ctx->prof_xchg += 1;
+            ctx->prof_xchg_exposed_ms += after;
             continue;
         }
-        if (ctx->evs[i].kind == kProfBoundary) {
+        if (kind == kProfBoundary) {
             ctx->prof_bnd_ms += ms;
             ctx->prof_bnd += 1;
+            ctx->prof_tail_ms += after;
             continue;
         }
         ctx->prof_ms += ms;
@@ -334,6 +345,7 @@ EventPair* next_event_pair(gol_ctx* ctx) {
     EventPair* ev = &ctx->evs[ctx->evs_used++];
     ev->kind = kProfMain;
     ev->clk_slot = -1;
+    ev->ref = -1;
     return ev;
 }
 
@@ -998,7 +1010,10 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         // complete instead of blocking in ncclGroupEnd until someone aborts
         // the communicator.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_ready, ctx->compute));
+        const size_t evs_before = ctx->evs_used;
         const int rc_interior = sharded_interior(ctx, G, slots, has_up, has_down);
+        // the interior launch's event pair (profiling; -1 if it has none in this fold window)
+        int iref = (ctx->prof && ctx->evs_used == evs_before + 1) ? (int)evs_before : -1;
         HIP_CHECK(ctx, hipStreamWaitEvent(ctx->comm, ctx->ev_ready, 0));
         const size_t cnt = (size_t)G * pitch;  // G contiguous rows (pitch padding included)
         // Issue order matters when up == down (2 ranks, or 1 rank sending to
@@ -1018,6 +1033,8 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
             xev = next_event_pair(ctx);
             if (!xev) return set_err(ctx, GOL_EHIP, "profiling event allocation failed");
             xev->kind = kProfExchange;
+            if ((int)ctx->evs_used - 1 <= iref) iref = -1;  // the allocation folded the window
+            xev->ref = iref;
             HIP_CHECK(ctx, hipEventRecord(xev->start, ctx->comm));
         }
         for (int k = 0; k < nops; ++k) (ops[k].send ? ctx->halo_sent : ctx->halo_recv) += ops[k].count * 4;
@@ -1034,8 +1051,12 @@ int one_pass(gol_ctx* ctx, int G, unsigned long long* slots) {
         // The event covers the sends too: the next pass overwrites this plane
         // only after the boundary kernels, which wait for it.
         HIP_CHECK(ctx, hipEventRecord(ctx->ev_halo, ctx->comm));
+        const size_t evs_mid = ctx->evs_used;
         int rc = sharded_boundary(ctx, G, slots, has_up, has_down, &ctx->ev_halo, 1);
         if (rc) return rc;
+        if (ctx->prof && ctx->evs_used == evs_mid + 1 && ctx->evs[evs_mid].kind == kProfBoundary && iref >= 0 &&
+            (int)evs_mid > iref)
+            ctx->evs[evs_mid].ref = iref;
     }
     ctx->cur ^= 1;
     ctx->epoch += (uint64_t)G;
@@ -1930,6 +1951,7 @@ int gol_profile_reset(gol_ctx* ctx) {
     ctx->prof_gens = 0;
     ctx->prof_clk_ms_ghz = ctx->prof_clk_ms = 0.0;
     ctx->prof_xchg_ms = ctx->prof_bnd_ms = 0.0;
+    ctx->prof_xchg_exposed_ms = ctx->prof_tail_ms = 0.0;
     ctx->prof_xchg = ctx->prof_bnd = 0;
     ctx->halo_sent = ctx->halo_recv = 0;
     return GOL_OK;
@@ -1950,6 +1972,8 @@ int gol_profile_stats_read(gol_ctx* ctx, gol_profile_stats* out) {
     out->halo_bytes_sent = ctx->halo_sent;
     out->halo_bytes_received = ctx->halo_recv;
     out->clock_ghz = ctx->prof_clk_ms > 0.0 ? ctx->prof_clk_ms_ghz / ctx->prof_clk_ms : 0.0;
+    out->exchange_exposed_ms = ctx->prof_xchg_exposed_ms;
+    out->pass_tail_ms = ctx->prof_tail_ms;
     return GOL_OK;
 }
 

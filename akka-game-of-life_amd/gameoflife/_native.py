@@ -66,6 +66,8 @@ class GolProfileStats(ctypes.Structure):
         ("halo_bytes_sent", ctypes.c_uint64),
         ("halo_bytes_received", ctypes.c_uint64),
         ("clock_ghz", ctypes.c_double),
+        ("exchange_exposed_ms", ctypes.c_double),
+        ("pass_tail_ms", ctypes.c_double),
     ]
 
 

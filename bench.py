@@ -560,7 +560,9 @@ def ring_stats(st, passes):
     """The self-ring windows' exchange figures (gol_profile_stats_read)."""
     n = max(st["exchanges"], 1)
     return {"exchange_ms_per_pass": round(st["exchange_ms"] / n, 4),
+            "exchange_exposed_ms_per_pass": round(st["exchange_exposed_ms"] / n, 4),
             "boundary_ms_per_pass": round(st["boundary_ms"] / max(st["boundary_launches"], 1), 4),
+            "pass_tail_ms_per_pass": round(st["pass_tail_ms"] / max(st["boundary_launches"], 1), 4),
             "halo_bytes_per_pass": round((st["halo_bytes_sent"] + st["halo_bytes_received"]) / max(passes, 1)),
             "passes": passes}
 
@@ -639,7 +641,8 @@ def rank_table(job, N, stats, dt, info):
     row = [round(dt * 1e9), round(stats["kernel_ms"] * 1e6), stats["launches"], round(stats["exchange_ms"] * 1e6),
            stats["exchanges"], round(stats["boundary_ms"] * 1e6), stats["boundary_launches"],
            stats["halo_bytes_sent"], stats["halo_bytes_received"], absorbed, info["hip_runtime_version"],
-           info["rccl_version"], lib_fingerprint(info)]
+           info["rccl_version"], lib_fingerprint(info), round(stats["exchange_exposed_ms"] * 1e6),
+           round(stats["pass_tail_ms"] * 1e6)]
     return job.gather(row)
 
 
@@ -767,6 +770,8 @@ def main():
                         "interior_ms_per_launch": [round(r[1] / 1e6 / max(r[2], 1), 4) for r in d],
                         "exchange_ms_per_pass": [round(r[3] / 1e6 / max(r[4], 1), 4) for r in d],
                         "boundary_ms_per_pass": [round(r[5] / 1e6 / max(r[6], 1), 4) for r in d],
+                        "exchange_exposed_ms_per_pass": [round(r[13] / 1e6 / max(r[4], 1), 4) for r in d],
+                        "pass_tail_ms_per_pass": [round(r[14] / 1e6 / max(r[6], 1), 4) for r in d],
                         "halo_bytes_per_pass": [round((r[7] + r[8]) / max(r[2], 1)) for r in d],
                         "passes": [r[2] for r in d],
                         "rccl_statuses_absorbed": [r[9] for r in d],
@@ -774,7 +779,9 @@ def main():
                         "rccl_version": [r[11] for r in d],
                         "note": "each rank's own timed window (clock stopped at its own sync; value uses the max); "
                                 "interior = the launch overlapping the exchange; exchange = comm-stream HIP events "
-                                "around the RCCL group, waiting for a late peer included"}
+                                "around the RCCL group, waiting for a late peer included; exposed / tail = how long "
+                                "after the interior launch the exchange / the boundary launch ended (the pass's "
+                                "critical path beyond the interior)"}
     if hashed is not None:
         out["with_state_hash"] = hashed
     if ring is not None:

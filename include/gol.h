@@ -312,7 +312,11 @@ int gol_profile_clock(gol_ctx* ctx, double* ghz);
  *   halo_bytes_sent / halo_bytes_received: bytes posted to / expected from
  *       the ring's send and receive operations (counted whether or not
  *       profiling is enabled);
- *   clock_ghz: as gol_profile_clock. */
+ *   clock_ghz: as gol_profile_clock;
+ *   exchange_exposed_ms / pass_tail_ms: per pass, how long after the end of
+ *       its interior launch the exchange (resp. the boundary launch) ended,
+ *       0 if before, summed: the part of the exchange the interior did not
+ *       hide, and the pass's whole critical path beyond the interior. */
 typedef struct gol_profile_stats {
     double kernel_ms;
     uint64_t launches;
@@ -324,6 +328,8 @@ typedef struct gol_profile_stats {
     uint64_t halo_bytes_sent;
     uint64_t halo_bytes_received;
     double clock_ghz;
+    double exchange_exposed_ms;  /* sum over passes of how long the exchange ended after the interior launch (>= 0) */
+    double pass_tail_ms;         /* ... and the boundary launch: the pass's critical path beyond the interior */
 } gol_profile_stats;
 int gol_profile_stats_read(gol_ctx* ctx, gol_profile_stats* out);
 

@@ -142,7 +142,9 @@ class FakeEngine:
                 "boundary_launches": self.launches if sharded else 0,
                 "halo_bytes_sent": 2 * 12 * self.w // 8 * self.launches if sharded else 0,
                 "halo_bytes_received": 2 * 12 * self.w // 8 * self.launches if sharded else 0,
-                "clock_ghz": 2.0}
+                "clock_ghz": 2.0,
+                "exchange_exposed_ms": 0.002 * self.launches if sharded else 0.0,
+                "pass_tail_ms": 0.004 * self.launches if sharded else 0.0}
 
     def occupancy(self, g):
         return (12 if g > 8 else 16), 124

@@ -86,8 +86,10 @@ def test_multirank_bench_line(tmp_path, world):
     assert len(set(settle_steps)) == 1 and settle_steps[0] >= 1
     # per-rank diagnostics gathered over the ring
     for key in ("interior_ms_per_launch", "exchange_ms_per_pass", "boundary_ms_per_pass", "halo_bytes_per_pass",
-                "passes", "rccl_statuses_absorbed", "hip_runtime_version", "rccl_version"):
+                "passes", "rccl_statuses_absorbed", "hip_runtime_version", "rccl_version",
+                "exchange_exposed_ms_per_pass", "pass_tail_ms_per_pass"):
         assert len(rk[key]) == world, key
+    assert rk["exchange_exposed_ms_per_pass"] == [0.002] * world and rk["pass_tail_ms_per_pass"] == [0.004] * world
     assert rk["halo_bytes_per_pass"] == [2 * 2 * 12 * 262144 // 8] * world
     assert rk["exchange_ms_per_pass"] == [0.05] * world and rk["rccl_statuses_absorbed"] == [0] * world
     rt = d["runtime"]

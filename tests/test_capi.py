@@ -127,14 +127,14 @@ def test_new_struct_layouts_match_header(tmp_path):
     src = tmp_path / "sz2.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "gol.h"\n'
                    'int main(void){printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(gol_profile_stats),'
-                   ' offsetof(gol_profile_stats, exchange_ms), offsetof(gol_profile_stats, clock_ghz),'
+                   ' offsetof(gol_profile_stats, exchange_ms), offsetof(gol_profile_stats, pass_tail_ms),'
                    ' sizeof(gol_runtime_info), offsetof(gol_runtime_info, rccl_library),'
                    ' offsetof(gol_runtime_info, gol_library)); return 0;}\n')
     exe = tmp_path / "sz2"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     assert got == [ctypes.sizeof(N.GolProfileStats), N.GolProfileStats.exchange_ms.offset,
-                   N.GolProfileStats.clock_ghz.offset, ctypes.sizeof(N.GolRuntimeInfo),
+                   N.GolProfileStats.pass_tail_ms.offset, ctypes.sizeof(N.GolRuntimeInfo),
                    N.GolRuntimeInfo.rccl_library.offset, N.GolRuntimeInfo.gol_library.offset]
 
 

@@ -47,6 +47,10 @@ def test_profile_stats_self_ring(gpu):
         assert st["exchanges"] == 3 and st["boundary_launches"] == 3
         assert st["halo_bytes_sent"] == 3 * 2 * G * pitch_bytes == st["halo_bytes_received"]
         assert st["kernel_ms"] > 0 and st["exchange_ms"] > 0 and st["boundary_ms"] > 0
+        # the exposed exchange and the boundary tail end after the interior
+        # launch by at most the whole exchange / boundary window
+        assert 0 <= st["exchange_exposed_ms"] <= st["exchange_ms"] + 1e-3
+        assert 0 <= st["pass_tail_ms"] and st["pass_tail_ms"] >= st["exchange_exposed_ms"] - 1e-3
         ms, n, g = e.profile_read()
         assert (ms, n, g) == (st["kernel_ms"], st["launches"], st["generations"])
         e.profile_reset()
