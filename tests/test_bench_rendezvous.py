@@ -1,0 +1,84 @@
+"""bench.py's torch-free rendezvous (CPU): rank 0's RCCL unique id travels
+through a file keyed by MASTER_ADDR:MASTER_PORT; a rank ignores a file older
+than its own start (minus two minutes of launch skew) -- the leftover of an
+earlier job on the same port -- and rank 0 removes the file once every rank
+has joined (after the first barrier over the new communicator)."""
+import os
+import threading
+import time
+import types
+
+import bench
+
+
+class _Eng:
+    def __init__(self):
+        self.joined = None
+        self.reduced = 0
+
+    def comm_init(self, uid, rank, world):
+        self.joined = (uid, rank, world)
+
+    def allreduce_u64(self, values):
+        self.reduced += 1
+        return values
+
+
+_N = types.SimpleNamespace(GOL_UNIQUE_ID_BYTES=128, unique_id=lambda: bytes(range(128)))
+
+
+def _job(monkeypatch, rank, port):
+    monkeypatch.setenv("RANK", str(rank))
+    monkeypatch.setenv("LOCAL_RANK", str(rank))
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(port))
+    return bench.Job(2)
+
+
+def test_rank0_publishes_then_removes(monkeypatch):
+    job = _job(monkeypatch, 0, 41001)
+    eng = _Eng()
+    path = job.uid_path()
+    job.join(eng, _N)
+    assert eng.joined == (bytes(range(128)), 0, 2) and eng.reduced == 1  # the barrier
+    assert not os.path.exists(path)
+
+
+def test_stale_file_is_ignored(monkeypatch):
+    job = _job(monkeypatch, 1, 41002)
+    path = job.uid_path()
+    with open(path, "wb") as f:
+        f.write(b"\x01" * 128)
+    old = time.time() - 3600
+    os.utime(path, (old, old))
+    fresh = bytes(range(128, 256))
+
+    def publish():
+        time.sleep(0.3)
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(fresh)
+        os.replace(tmp, path)
+
+    t = threading.Thread(target=publish)
+    t.start()
+    eng = _Eng()
+    job.join(eng, _N, timeout=20)
+    t.join()
+    assert eng.joined == (fresh, 1, 2)
+    os.unlink(path)
+
+
+def test_gather_lays_rows_by_rank(monkeypatch):
+    job = _job(monkeypatch, 1, 41003)
+
+    class Sum(_Eng):
+        def allreduce_u64(self, values):
+            import numpy as np
+            v = np.asarray(values, dtype=np.uint64).copy()
+            v[:3] += np.array([7, 8, 9], dtype=np.uint64)  # rank 0's row
+            return v
+
+    job.eng = Sum()
+    assert job.gather([1, 2, 3]) == [[7, 8, 9], [1, 2, 3]]
