@@ -34,10 +34,15 @@ def dispatches(path):
 
 def pick(ds, n, k):
     """The timed launches of window k: the last n step-kernel dispatches
-    before the k-th gol_hash (hash_kernel) of the run -- bench.py hashes the
-    board right after each window for its parity check (rocprofv3 -T truncates
-    the kernel names to their base names, so the order is the key)."""
-    hashes = [i for i, e in enumerate(ds) if e["name"].startswith("hash_kernel")]
+    before the k-th gol_hash (hash_kernel) of the headline board -- bench.py
+    hashes the board right after each window for its parity check.  Round 4
+    checks the 65536^2 windows too, so only the hashes of the 16x larger
+    262144^2 board count (the hash grid is capped, so it is told apart by its
+    duration).  (rocprofv3 -T truncates the kernel names to their base
+    names, so the order is the key.)"""
+    hs = [i for i, e in enumerate(ds) if e["name"].startswith("hash_kernel")]
+    longest = max(ds[i]["t"] for i in hs)
+    hashes = [i for i in hs if ds[i]["t"] >= 0.5 * longest]
     end = hashes[k]
     steps = [i for i in range(end) if e_is_step(ds[i])]
     return [ds[i] for i in steps[-n:]]

@@ -67,46 +67,58 @@ def main():
     lines += ["", "bench.py HIP-event numbers from the same run (timed region only) beside the trace:"]
 
     def instance(G, hashed):
-        # multistep_hg_kernel<2, G, LIFE, HASH, torus, pairs> (step_kernel<2, ...> at G = 1)
+        # multistep_hg_kernel<2, G, LIFE, HASH, torus, ILV = 2> (step_kernel<4, ...> at G = 1)
         h = "true" if hashed else "false"
         if G == 1:
-            return f"step_kernel<2, true, {h}, false, true>"
-        return f"multistep_hg_kernel<2, {G}, true, {h}, false, true>"
+            return f"step_kernel<4, true, {h}, false, 2>"
+        return f"multistep_hg_kernel<2, {G}, true, {h}, false, 2>"
 
-    def traced(plan, hashed, warmup):
-        # The timed launches of a run: in dispatch order, each depth's first
-        # launches at the largest grid of its instance (the whole-board
-        # launch), after the warm-up's single pass of `warmup` generations
-        # (gol_step plans <= 12 generations as one pass).  Returns (mean of
-        # the timed launches, mean over every launch of those instances).
-        seen = defaultdict(int)
-        if warmup and warmup <= 12:
-            seen[warmup] = 1
-        timed, every = [], []
-        for G in plan:
-            cands = [(gx, d) for (name, gx, gy), d in groups.items() if instance(G, hashed) in name]
-            if not cands:
-                return None, None
-            gx, d = max(cands, key=lambda c: c[0])
-            if seen[G] >= len(d):
-                return None, None
-            timed.append(d[seen[G]])
-            seen[G] += 1
-            every.append(statistics.mean(d))
-        return statistics.mean(timed), statistics.mean(every)
+    # Dispatches in time order.  Round 4's window (bench.py fresh_window):
+    # seed, untimed settle passes, seed again, the warm-up pass, the timed
+    # passes; the hashed window follows with no seed.  The timed launches are
+    # found by walking the trace from the main board's second seed.
+    order = [(r["Kernel_Name"], int(r["Grid_Size_X"]),
+              (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6) for r in trace]
+    big_seed = max((gx for n, gx, _ in order if "seed_kernel" in n), default=0)
+    seeds = [i for i, (n, gx, _) in enumerate(order) if "seed_kernel" in n and gx == big_seed]
 
-    for label, rec, hashed in (("main workload", b, False), ("with_state_hash", b.get("with_state_hash"), True)):
+    def whole_board(G, hashed):
+        cands = [gx for (name, gx, gy) in groups if instance(G, hashed) in name]
+        return max(cands) if cands else None
+
+    def walk(start, plan, hashed, warmup):
+        """Durations of the timed launches after dispatch `start` (the warm-up
+        pass first, when there is one), and the index after them."""
+        i, out = start, []
+        steps = ([warmup] if warmup and warmup <= 12 else []) + list(plan)
+        for k, G in enumerate(steps):
+            gx = whole_board(G, hashed)
+            if gx is None:
+                return None, start
+            while i < len(order) and not (instance(G, hashed) in order[i][0] and order[i][1] == gx):
+                i += 1
+            if i == len(order):
+                return None, start
+            if k >= len(steps) - len(plan):
+                out.append(order[i][2])
+            i += 1
+        return out, i
+
+    main_t, after = walk(seeds[1], b.get("pass_plan") or b["roofline"].get("pass_plan"), False,
+                         b.get("warmup")) if len(seeds) > 1 else (None, 0)
+    hrec = b.get("with_state_hash")
+    hash_t = walk(after, hrec["pass_plan"], True, b.get("warmup"))[0] if hrec and main_t else None
+    for label, rec, t in (("main workload", b, main_t), ("with_state_hash", hrec, hash_t)):
         if not rec or not rec.get("roofline"):
             continue
         ro = rec["roofline"]
-        plan = rec.get("pass_plan") or ro.get("pass_plan") or b.get("pass_plan")
-        t, t_all = traced(plan, hashed, b.get("warmup")) if plan else (None, None)
         lines.append(f"  {label:16s} bench avg_launch_ms={ro.get('avg_launch_ms')} launches={ro.get('launches')}"
-                     + (f"   rocprof, the same timed launches: mean={t:.4f} ms"
-                        f" (every launch of those instances and grids: {t_all:.4f} ms)" if t else ""))
-    lines.append("(the timed launches are picked from the trace in dispatch order: each pass depth's first")
-    lines.append(" whole-board launches after the warm-up pass; the instances' later launches at the same grid")
-    lines.append(" belong to the N = 1 ring-schedule runs on a settled, sparser board)")
+                     + (f"   rocprof, the same timed launches: mean={statistics.mean(t):.4f} ms "
+                        f"({', '.join(f'{x:.4f}' for x in t)})" if t else ""))
+    lines.append("(the timed launches are picked from the trace in dispatch order: from the main board's second")
+    lines.append(" seed (the re-seed after the untimed settle), the warm-up pass, then the timed passes; the")
+    lines.append(" hashed window's follow them; the instances' other launches at the same grids are the settle")
+    lines.append(" passes and the N = 1 ring-schedule runs)")
     with open(os.path.join(dst, f"{tag}_kernel_trace.txt"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("\n".join(lines))
