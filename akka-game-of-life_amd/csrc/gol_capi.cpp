@@ -1157,35 +1157,29 @@ int depth_cap(const gol_ctx* ctx) {
 }
 
 // Pass planner (DESIGN.md section 4 "Pass planner").  Relative time of one
-// pass of G generations (G = 1..12, G = 6 -> 1) on the multi-generation
-// kernels, from scripts/depth_sweep.py (profiles/r01_depth_sweep.txt, two
-// boxes): up to G = 6 a pass costs about the same (the sweep over the plane
-// is HBM-bound), deeper passes cost more but less per generation on wide
-// boards (>= 32 column strips); narrow boards are best at 8.
-// G = 9..12 (round 2, 3 waves/SIMD at G >= 10): fresh-board depth sweep
-// (profiles/r02_depth_sweep_deep.txt) calibrated by same-box pass mixes
-// (profiles/r02_plan_mix_ab.txt: 20 generations 12 + 8 at 111.1k GCUPS vs
-// 6 + 6 + 8 at 103.6k; 60 generations 5 x 12 at 119.0k vs 6 x 10 at 115.0k).
-// With the fused per-generation hash the kernels are VALU-bound from G = 6
-// on.  The hashed B3/S23 instances skip the dead pipeline-fill steps up to
-// G = 12 (row step force-inlined: 153 / 163 / 168 VGPRs at G = 10 / 11 / 12,
-// 3 waves per SIMD, G = 12 with a 7-dword spill), so on wide boards G = 10
-// and 11 are best per generation (same-box sweep, profiles/r02_hash_deep_ab.txt:
-// 0.72 / 0.70 ms per generation at 262144^2 vs 0.73 at G = 8; 20 generations
-// as 10 + 10 94.5k vs 7 + 7 + 6 90.4k GCUPS); narrow boards stay at 8
-// (HASH=1 rows; profiles/r02_hash_peel_ab.txt, r02_hash_deep_ab.txt).
+// pass of G generations (G = 1..12, G = 6 -> 1), from scripts/depth_sweep.py
+// (min of 3 rounds, reseeded board) on the row-pair-shared B3/S23 kernels
+// (profiles/r04_pair_depth_sweep.txt; round 4).  Up to G = 6 a pass costs
+// about the same (the sweep over the plane is HBM-bound); deeper passes cost
+// more but less per generation.  The paired kernels hold 3 waves per SIMD up
+// to G = 10 and 2 at G = 11 and 12 (rings of 174-197 VGPRs), so G = 10 is the
+// cheapest per generation on both wide (>= 32 column strips) and narrow
+// boards, unhashed and hashed, except narrow hashed boards where G = 7 ties it.
+// Earlier rounds' per-row circuit tables: profiles/r01_depth_sweep.txt,
+// r02_depth_sweep_deep.txt, r02_hash_deep_ab.txt.
 constexpr double kPassCost[2][2][gol::kMaxGensPerPass + 1] = {
     // [hashed][wide]; G = 0 .. 12
-    {{0, 0.817, 0.926, 0.943, 0.967, 0.957, 1.00, 1.20, 1.26, 1.457, 1.657, 1.829, 1.995},    // narrow (G 7/8: XCD block order, r01_depth_sweep_xcd + r01_plan65_ab)
-     {0, 0.80, 1.056, 1.075, 1.06, 1.04, 1.00, 1.136, 1.231, 1.37, 1.52, 1.70, 1.77}},        // wide (G 7/8: same-box pass mixes, r01_plan_mix_ab)
-    {{0, 0.683, 0.771, 0.791, 0.846, 0.884, 1.00, 1.09, 1.20, 1.49, 1.60, 1.75, 2.49},        // narrow, hashed (65536^2)
-     {0, 0.728, 0.852, 0.861, 0.863, 0.869, 1.00, 1.08, 1.22, 1.40, 1.51, 1.63, 1.97}}};      // wide, hashed (262144^2)
+    {{0, 0.755, 0.984, 0.995, 0.987, 0.964, 1.00, 1.068, 1.274, 1.346, 1.459, 1.893, 2.022},   // narrow (65536^2)
+     {0, 0.739, 1.084, 1.088, 1.045, 1.020, 1.00, 1.073, 1.223, 1.340, 1.446, 1.696, 1.809}},  // wide (262144^2)
+    {{0, 0.642, 0.846, 0.859, 0.880, 0.894, 1.00, 1.077, 1.353, 1.449, 1.553, 2.109, 2.256},   // narrow, hashed
+     {0, 0.615, 0.904, 0.908, 0.883, 0.861, 1.00, 1.084, 1.278, 1.382, 1.496, 1.806, 1.941}}}; // wide, hashed
 
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);
 // otherwise the plan minimises the summed pass cost (a DP over n, n <= 1024:
 // callers plan per chunk), deepest passes first (12 + 8 ran 3 % faster than
-// 8 + 12 from the bench's fresh board, profiles/r02_plan_mix_ab.txt).
+// 8 + 12 from the bench's fresh board with the per-row circuit,
+// profiles/r02_plan_mix_ab.txt).
 // Deterministic in (width, height, N, n), so all shards of a ring plan alike.
 std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n, bool hashed) {
     const int cap = depth_cap(ctx);

@@ -306,6 +306,46 @@ __device__ __forceinline__ uint32_t rule_b3s23_fullsum(uint32_t a0, uint32_t a1,
     return GOL_BITOP3(e2, f1, t2, kRuleOut);
 }
 
+// Row-pair-shared B3/S23 (multistep_hg_kernel on tori).  Output rows m and
+// m + 1 (m even) both sum h(m) + h(m + 1); their binary sum P (0..6, three
+// planes) is formed once and each row adds its own third h:
+//   S(m) = h(m - 1) + P,  S(m + 1) = P + h(m + 2).
+// The 4-gate tail takes P, the third row's (x1 x0) and the centre; it was
+// found by exhaustive search over 4-gate 3-input circuits on the binary P
+// (DESIGN.md §4 "Rule circuit"; none of 3 gates exists for any 3-plane code of
+// P, and no 3-gate sum of a + b separates its values), and is checked on
+// every input by tests/test_rule_circuit.py.  Per two rows: 4 + 2 x 4 gates
+// instead of 2 x 7.
+constexpr uint32_t kPairT1 = 0x43;
+constexpr uint32_t kPairT2 = 0x18;
+constexpr uint32_t kPairT3 = 0x26;
+constexpr uint32_t kPairOut = 0xD0;
+
+template <int VEC>
+struct PairSum {
+    uint32_t p0[VEC], p1[VEC], p2[VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ void pair_sum(const uint32_t (&a0)[VEC], const uint32_t (&a1)[VEC],
+                                         const uint32_t (&b0)[VEC], const uint32_t (&b1)[VEC], PairSum<VEC>& P) {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+        const uint32_t k = a0[j] & b0[j];
+        P.p0[j] = a0[j] ^ b0[j];
+        P.p1[j] = GOL_BITOP3(a1[j], b1[j], k, kXor3);
+        P.p2[j] = GOL_BITOP3(a1[j], b1[j], k, kMaj);
+    }
+}
+
+__device__ __forceinline__ uint32_t rule_b3s23_pair(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t x0, uint32_t x1,
+                                                    uint32_t alive) {
+    const uint32_t g1 = GOL_BITOP3(p0, x0, alive, kPairT1);
+    const uint32_t g2 = GOL_BITOP3(p1, p2, g1, kPairT2);
+    const uint32_t g3 = GOL_BITOP3(p2, x1, g2, kPairT3);
+    return GOL_BITOP3(g3, alive, g1, kPairOut);
+}
+
 // Column sums of the visible rows: (v1 v0) = a + c + b (the full 3-cell
 // column, seen by the columns left and right of it) and (p1 p0) = a + b (the
 // column minus its centre, seen by the centre cell itself).
@@ -907,13 +947,28 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
 #ifndef GOL_HG_MINWAVES_QUAD
 #define GOL_HG_MINWAVES_QUAD 2
 #endif
-template <int VEC, int G, bool LIFE, bool HASH>
-constexpr int kHgMinWaves = (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8
+// The horizontal-first B3/S23 torus kernels share each even/odd row pair's
+// middle sum (rule_b3s23_pair); -DGOL_PAIR_ROWS=0 builds the per-row circuit.
+#ifndef GOL_PAIR_ROWS
+#define GOL_PAIR_ROWS 1
+#endif
+// Quad lanes (VEC = 4) keep the per-row circuit: the paired 8-generation
+// instance spills at 256 VGPRs.
+template <int VEC, bool LIFE, bool CLIPPED>
+constexpr bool kPairRows = GOL_PAIR_ROWS && LIFE && !CLIPPED && VEC <= 2;
+
+// The row-pair-shared instances (kPairRows) run at the occupancy their
+// registers give (G <= 10: 3 or more waves per SIMD): forced to the limits
+// above they spill (8 generations hashed: 40 bytes per lane).
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
+constexpr int kHgMinWaves = (VEC == 4) ? GOL_HG_MINWAVES_QUAD
+                             : kPairRows<VEC, LIFE, CLIPPED> ? 1
+                             : (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8
                              : (VEC == 2 && G >= 10 && LIFE && HASH) ? GOL_HG_MINWAVES_DEEP
-                             : (VEC == 4) ? GOL_HG_MINWAVES_QUAD : 1;
+                             : 1;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
-__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH>)) void multistep_hg_kernel(
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH, CLIPPED>)) void multistep_hg_kernel(
     const StepParams p) {
     constexpr int HG = kHashGroup<ILV>;
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
@@ -983,6 +1038,11 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 
         Words<VEC> in[kMRing];
         HRow<VEC, CLIPPED> hr[G][3];  // ring s: arrivals of stage-s rows (stage 0 = input), slot = row % 3
+        PairSum<VEC> pst[kPairRows<VEC, LIFE, CLIPPED> ? G : 1];  // stage s's last even-row P
+#pragma unroll
+        for (int s = 0; s < (kPairRows<VEC, LIFE, CLIPPED> ? G : 1); ++s)
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) pst[s].p0[j] = pst[s].p1[j] = pst[s].p2[j] = 0u;
 #pragma unroll
         for (int k = 0; k < kMRing; ++k)
 #pragma unroll
@@ -1029,13 +1089,32 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
             arrive<VEC, CLIPPED, ILV>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
             for (int s = 1; s <= G; ++s) {
-                if (fill && q < 2 * s) break;  // stages s.. have no valid row yet
+                // stages s.. have no valid row yet; a paired stage also runs the
+                // step before its first valid row, to form that row's P when odd
+                if (fill && q < 2 * s - (kPairRows<VEC, LIFE, CLIPPED> ? 1 : 0)) break;
                 // stage s: stream row m = q - s from ring s-1 rows m-1, m, m+1
                 const int m = q - s;
                 Words<VEC> o;
-                rule_hg<VEC, LIFE, CLIPPED>(p, hr[s - 1][((u - s - 1) % 3 + 3) % 3],
-                                            hr[s - 1][((u - s) % 3 + 3) % 3],
-                                            hr[s - 1][((u - s + 1) % 3 + 3) % 3], omask, o);
+                const HRow<VEC, CLIPPED>& A = hr[s - 1][((u - s - 1) % 3 + 3) % 3];
+                const HRow<VEC, CLIPPED>& C = hr[s - 1][((u - s) % 3 + 3) % 3];
+                const HRow<VEC, CLIPPED>& B = hr[s - 1][((u - s + 1) % 3 + 3) % 3];
+                if constexpr (kPairRows<VEC, LIFE, CLIPPED>) {
+                    // q - u is a multiple of kMRing (even), so m's parity is u - s's
+                    if (((u - s) & 1) == 0) {
+                        pair_sum<VEC>(C.h0, C.h1, B.h0, B.h1, pst[s - 1]);  // h(m) + h(m + 1)
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j)
+                            o.w[j] = rule_b3s23_pair(pst[s - 1].p0[j], pst[s - 1].p1[j], pst[s - 1].p2[j],
+                                                     A.h0[j], A.h1[j], C.r[j]);
+                    } else {  // h(m - 1) + h(m), formed by the even row before
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j)
+                            o.w[j] = rule_b3s23_pair(pst[s - 1].p0[j], pst[s - 1].p1[j], pst[s - 1].p2[j],
+                                                     B.h0[j], B.h1[j], C.r[j]);
+                    }
+                } else {
+                    rule_hg<VEC, LIFE, CLIPPED>(p, A, C, B, omask, o);
+                }
                 const bool own_row = m >= G && m < n_in - G;
                 if constexpr (HASH) {
 #if GOL_HASH_LDS

@@ -63,12 +63,18 @@ DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass
 
 # Issue-cost model of the multi-generation kernel's loop (DESIGN.md "Roofline"):
 # VALU instructions per 32-cell word and generation of multistep_hg_kernel<2, G,
-# LIFE> on the pair layout (scripts/isa_loop.py census: at G = 6, 800 VALU per
-# 6-row unroll = 648 bitop3 + 72 alignbit + 72 DPP + loop overhead) and the
-# measured cycles per wave64 instruction on one SIMD (profiles/r01_valu_op_costs.txt).
-VALU_MIX = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
-# The quad layout (4 interleaved words per lane): one
-# funnel shift and one DPP move per quad edge, i.e. half of each per word.
+# LIFE> on the pair layout and the measured cycles per wave64 instruction on one
+# SIMD (profiles/r01_valu_op_costs.txt).  Round 4's row-pair-shared circuit
+# (gol_stencil.h rule_b3s23_pair): per word-generation 2 bitop3 for the row's
+# horizontal sum, half of the pair sum P (1 bitop3 + 1 v_xor + 1 v_and per two
+# rows) and a 4-bitop3 tail, plus one funnel shift and one DPP move
+# (scripts/isa_loop.py census of the G = 12 loop: 6.54 bitop3 and
+# 0.47 v_xor + 0.47 v_and per v_alignbit, the (G + 1) / G arrivals included).
+VALU_MIX = {"v_bitop3_b32": (7, 2.3), "v_xor_b32": (0.5, 2.3), "v_and_b32": (0.5, 2.3),
+            "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
+# The quad layout (4 interleaved words per lane) keeps the
+# per-row 9-bitop3 circuit; one funnel shift and one DPP move per quad edge,
+# i.e. half of each per word.
 VALU_MIX_QUAD = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (0.5, 4.1), "v_mov_b32_dpp": (0.5, 4.3)}
 # The fused hash adds one v_mad_u64_u32 per word and generation (DESIGN.md "State hash").
 VALU_MIX_HASH = dict(VALU_MIX, v_mad_u64_u32=(1, 4.6))
@@ -78,7 +84,7 @@ VALU_MIX_QUAD_HASH = dict(VALU_MIX_QUAD, v_mad_u64_u32=(1, 4.6))
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: 60 timed generations = 2 x 6 + 6 x 8 passes at 262144^2 (the planner's choice)
+    # defaults: 60 timed generations = 6 x 10 passes at 262144^2 (the planner's choice)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--board", type=int, default=262144, help="board edge (cells)")

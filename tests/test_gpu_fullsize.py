@@ -1,14 +1,15 @@
 """GPU parity at the sizes and pass plans the benchmark times.
 
 * 262144^2 torus (BASELINE.json configs[3], 8 GiB per plane), 20 generations
-  -- the driver's `bench.py --steps 20`: unhashed the planner runs 12 + 8
-  (the wide G = 12 and G = 8 instances of multistep_hg_kernel, tail split
-  active at >= 32 strips), hashed the planner's hashed plan (10 + 10).
+  -- the driver's `bench.py --steps 20`: the planner runs 10 + 10 unhashed
+  and hashed (the wide G = 10 instances of multistep_hg_kernel with the
+  row-pair-shared circuit, tail split active at >= 32 strips).
   As one context (N = 1), as an in-process group of 8 row shards of 32768 rows (the N = 8 decomposition:
   interior launch + boundary rows on the edge stream), and as a 1-rank RCCL
   self-ring (the ring schedule's ncclSend / ncclRecv).
 * 65536^2 torus (configs[2]), 102 generations -- the kernels and pass depth
-  of the bench's secondary run (12 x 8 + 6 unhashed; the bench times 128 x 8).
+  of the bench's secondary run (7 x 10 + 2 x 9 + 2 x 7 unhashed; the bench
+  times 101 x 10 + 2 x 7).
 * 262144 x 16384: the benchmark's own unhashed path on a board of 67 strips
   with more than one round of resident waves (bulk bands + tail bands).
 
@@ -46,7 +47,7 @@ def _unhashed_then_check(e, final, want_last):
 def test_full_size_262144_plans_are_the_benchs(gpu):
     from gameoflife.engine import GolEngine
     with GolEngine(W, H) as e:
-        assert e.pass_plan(GENS) == [12, 8]
+        assert e.pass_plan(GENS) == [10, 10]
         assert e.pass_plan(GENS, hashes=True) == [10, 10]
 
 
@@ -108,14 +109,15 @@ def test_full_size_262144_eight_shards(gpu, oracle_run):
 
 def test_full_size_65536_bench_plan(gpu):
     """configs[2]: the bench's secondary run's kernels, 102 generations
-    (unhashed 12 x 8 + 6), final board and hash; hashed, every generation's hash."""
+    (unhashed 7 x 10 + 2 x 9 + 2 x 7), final board and hash; hashed, every
+    generation's hash."""
     from gameoflife.engine import GolEngine
     S, n = 65536, 102
     board = O.seed_packed(S, S, 0x5EED)
     final, want = O.run_packed(board, S, n, O.TORUS, O.LIFE)
     del board
     with GolEngine(S, S) as e:
-        assert e.pass_plan(n) == [8] * 12 + [6]
+        assert e.pass_plan(n) == [10] * 7 + [9, 9, 7, 7]
         e.seed(0x5EED)
         e.step(n)
         assert e.hash() == int(want[-1])
@@ -152,7 +154,7 @@ def test_wide_board_several_rounds_unhashed(gpu):
     board = O.seed_packed(Wd, Hd, 77)
     final, want = O.run_packed(board, Wd, n, O.TORUS, O.LIFE)
     with GolEngine(Wd, Hd) as e:
-        assert e.pass_plan(n) == [12, 8]
+        assert e.pass_plan(n) == [10, 10]
         e.load(board)
         e.step(n)
         assert e.hash() == int(want[-1])

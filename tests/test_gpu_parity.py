@@ -342,22 +342,23 @@ def test_known_patterns_on_gpu(gpu):
 def test_pass_plan(gpu):
     """gol_pass_plan: the depths cover the generations exactly, respect the
     cap (12 on the B3/S23 torus, 8 for other rules and the clipped topology,
-    or a fixed gens_per_pass), run deepest first, and wide boards fuse deeper
-    passes (DESIGN.md "Pass planner")."""
-    with engine(32 * 300, 64) as e:  # narrow (3 strips): 8-generation passes
+    or a fixed gens_per_pass), run deepest first, and follow the cost table
+    (DESIGN.md "Pass planner")."""
+    with engine(32 * 300, 64) as e:  # narrow (3 strips): 10-generation passes (round-4 paired kernels)
         for n in (1, 5, 6, 7, 13, 50, 60, 1024):
             plan = e.pass_plan(n)
             assert sum(plan) == n and all(1 <= g <= 12 for g in plan), (n, plan)
             assert plan == sorted(plan, reverse=True), plan
-        assert e.pass_plan(48) == [8] * 6
-        assert e.pass_plan(102) == [8] * 12 + [6]
-        assert e.pass_plan(60, hashes=True) == [8] * 4 + [7] * 4  # hashed: VALU-bound, 7-8 are best
+        assert e.pass_plan(48) == [10] * 3 + [9] * 2
+        assert e.pass_plan(102) == [10] * 7 + [9, 9, 7, 7]
+        assert e.pass_plan(60, hashes=True) == [10] * 6
         e.set_tuning(gens_per_pass=4)
         assert e.pass_plan(10) == [4, 4, 2]
-    with engine(262144, 64) as e:  # wide (67 strips): 12-generation passes
-        assert e.pass_plan(60) == [12] * 5
-        assert e.pass_plan(20) == [12, 8]
-        assert e.pass_plan(60, hashes=True) == [11] * 4 + [8] * 2  # hashed: 10-11 best (3 waves/SIMD)
+    with engine(262144, 64) as e:  # wide (67 strips): G = 10, the deepest paired kernel at 3 waves/SIMD
+        assert e.pass_plan(60) == [10] * 6
+        assert e.pass_plan(20) == [10, 10]
+        assert e.pass_plan(12) == [12]
+        assert e.pass_plan(60, hashes=True) == [10] * 6
         assert e.pass_plan(20, hashes=True) == [10, 10]
         check = e.pass_plan(13)
         assert sum(check) == 13
