@@ -1319,6 +1319,10 @@ int gol_create(gol_ctx** out, const gol_config* cfg) {
     if (c.width <= 0 || c.height <= 0) return set_err(nullptr, GOL_EINVAL, "width/height must be > 0");
     if (c.topology != GOL_TORUS && c.topology != GOL_REF_CLIPPED)
         return set_err(nullptr, GOL_EINVAL, "unknown topology %d", c.topology);
+    // Column indices in the kernels (StepParams.wwords, lane columns) are
+    // int32 word counts: rows below 2^31 cells keep them far inside range.
+    if (c.width >= (int64_t(1) << 31))
+        return set_err(nullptr, GOL_EINVAL, "width must be below 2^31 cells (got %lld)", (long long)c.width);
     if (c.topology == GOL_TORUS && c.width % 32 != 0)
         return set_err(nullptr, GOL_EINVAL, "torus width must be a multiple of 32 (got %lld)", (long long)c.width);
     if ((c.birth_mask | c.survive_mask) & ~0x1FFu)

@@ -74,7 +74,7 @@ typedef struct gol_ctx gol_ctx;
  * placement (BoardCreator.scala:65-70): a context owns the row block
  * [row0, row0 + rows) of a width x height board. */
 typedef struct gol_config {
-    int64_t width;          /* cells per row (torus: multiple of 32)          */
+    int64_t width;          /* cells per row (torus: multiple of 32), < 2^31  */
     int64_t height;         /* rows of the global board                       */
     int64_t row0;           /* first global row owned by this context         */
     int64_t rows;           /* rows owned (0 => height - row0)                */

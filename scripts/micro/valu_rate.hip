@@ -21,6 +21,10 @@ constexpr int kIters = 4096;
 //           quad 2 DPP + 2 v_alignbit + 8 + 4 x 7 v_bitop3 = 40 ops (MODE 4:
 //           44 for two pairs).
 //   MODE 7: MODE 6 with ds_bpermute one row ahead.
+//   MODE 8: the row-pair-shared circuit (rule_b3s23_pair): two rows of a pair
+//           arrive (per row 2 DPP + 2 v_alignbit + 4 v_bitop3), their P is formed
+//           per word (v_xor + v_and + 2 v_bitop3) and each of the 2 x 2 words
+//           runs the 4-v_bitop3 tail: 40 VALU per 4 word-generations.
 __device__ __forceinline__ uint32_t rule7(uint32_t a0, uint32_t a1, uint32_t c0, uint32_t c1, uint32_t b0, uint32_t b1,
                                           uint32_t alive) {
     const uint32_t e1 = __builtin_amdgcn_bitop3_b32(a0, c0, b0, 0x69);
@@ -122,6 +126,40 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
                     pl[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_l, (int)(kQuad ? (c[i] ^ a[i]) : b[i]));
                     pr[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_r, (int)a[i]);
                 }
+            } else if constexpr (MODE == 8) {
+                uint32_t hh0[2][2], hh1[2][2], rr[2][2];
+                uint32_t rows[2][2] = {{a[i], b[i]}, {d[i], c[i] ^ a[i]}};
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t e = rows[r][0], o = rows[r][1];
+                    const uint32_t left = (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x138, 0xf, 0xf, true);
+                    const uint32_t right = (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x130, 0xf, 0xf, true);
+                    const uint32_t we = __builtin_amdgcn_alignbit(o, left, 31);
+                    const uint32_t eo = __builtin_amdgcn_alignbit(right, e, 1);
+                    hh0[r][0] = __builtin_amdgcn_bitop3_b32(we, e, o, 0x96);
+                    hh1[r][0] = __builtin_amdgcn_bitop3_b32(we, e, o, 0xe8);
+                    hh0[r][1] = __builtin_amdgcn_bitop3_b32(e, o, eo, 0x96);
+                    hh1[r][1] = __builtin_amdgcn_bitop3_b32(e, o, eo, 0xe8);
+                    rr[r][0] = e; rr[r][1] = o;
+                }
+                uint32_t out4[2][2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t k = hh0[0][j] & hh0[1][j];
+                    const uint32_t p0 = hh0[0][j] ^ hh0[1][j];
+                    const uint32_t p1 = __builtin_amdgcn_bitop3_b32(hh1[0][j], hh1[1][j], k, 0x96);
+                    const uint32_t p2 = __builtin_amdgcn_bitop3_b32(hh1[0][j], hh1[1][j], k, 0xe8);
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {  // x: the chain's previous rows (c: above, pl: below)
+                        const uint32_t x0 = r ? pl[i] : c[i], x1 = r ? pr[i] : (c[i] ^ 0x5a5a5a5au), al = rr[r][j];
+                        const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, x0, al, 0x43);
+                        const uint32_t g2 = __builtin_amdgcn_bitop3_b32(p1, p2, g1, 0x18);
+                        const uint32_t g3 = __builtin_amdgcn_bitop3_b32(p2, x1, g2, 0x26);
+                        out4[r][j] = __builtin_amdgcn_bitop3_b32(g3, al, g1, 0xd0);
+                    }
+                }
+                c[i] = hh0[1][0]; pl[i] = hh0[0][1]; pr[i] = hh1[1][1];
+                a[i] = out4[0][0]; b[i] = out4[0][1]; d[i] = out4[1][0] ^ out4[1][1];
             } else {  // step-kernel mix: 1 DPP, 2 alignbit, 9 bitop3, 1 xor  (13)
                 const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[i], 0x138, 0xf, 0xf, true);
                 const uint32_t w = __builtin_amdgcn_alignbit(a[i], l, 31);
@@ -182,6 +220,17 @@ int main() {
     uint32_t* out; unsigned long long* clk;
     CHK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4)); CHK(hipMalloc(&clk, 16));
     const bool r3 = getenv("VALU_RATE_R3") != nullptr;  // only the round-3 loop mix, at 1..8 waves/SIMD
+    if (getenv("VALU_RATE_PAIR")) {
+        // the per-row circuit (MODE 4, 22 VALU per 2 word-generations) beside
+        // the row-pair-shared one (MODE 8, 40 VALU per 4 word-generations)
+        for (int w : {2, 3, 4}) {
+            run<4, 2>("per-row circuit (22 VALU/pair)", 22, w, out, clk, cus, 2);
+            run<4, 4>("per-row circuit (22 VALU/pair)", 22, w, out, clk, cus, 2);
+            run<8, 1>("pair-row circuit (40 VALU/2 pairs)", 40, w, out, clk, cus, 4);
+            run<8, 2>("pair-row circuit (40 VALU/2 pairs)", 40, w, out, clk, cus, 4);
+        }
+        return 0;
+    }
     if (getenv("VALU_RATE_R4")) {
         // word-generations per cycle per SIMD: a pair iteration advances 2
         // words, a quad iteration 4 (the ops column counts VALU only)

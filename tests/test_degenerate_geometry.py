@@ -78,3 +78,16 @@ def test_torus_tiny_boards_still_accepted():
             GolEngine(32, H, topology="torus").close()
         except N.GolError as e:
             assert e.code == N.GOL_ENODEV
+
+
+def test_width_beyond_int32_rows_refused():
+    """Kernel row pitches are 32-bit word counts: gol_create refuses rows of
+    2^31 cells or more before it looks for a device."""
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    for W in (1 << 31, 1 << 40):
+        try:
+            GolEngine(W, 1, topology="torus").close()
+            raise AssertionError("accepted")
+        except N.GolError as e:
+            assert e.code == N.GOL_EINVAL and "2^31" in str(e)
