@@ -14,4 +14,6 @@ for counters in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY 
   timeout -s KILL 90 rocprofv3 --pmc $counters -T -d $P/pass$i -o run --output-format csv -- python3 scripts/prof_run.py 262144x262144 10 > $P/pass$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $P/pass$i.log; exit $rc; }
 done
-VALU_RATE_PAIR=1 timeout -k 10 60 scripts/micro/valu_rate > gpurun_out/sq/valu_rate_pair.txt 2>&1
+VALU_RATE_PAIR=1 timeout -k 10 60 scripts/micro/valu_rate > gpurun_out/sq/valu_rate_pair.txt 2>&1 || exit 1
+# the N = 2 / 4 per-rank ring shapes at the planner's depth (pmc_launch.json rows)
+CONFIGS="262144x131072:ring:10:0 262144x65536:ring:10:0 262144x32768:ring:10:1" bash scripts/gpu_pmc.sh > gpurun_out/pmc_r4ring.log 2>&1
