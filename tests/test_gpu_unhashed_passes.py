@@ -67,6 +67,18 @@ def test_strip_geometry(gpu):
         assert e.occupancy(12)[1] == 62
 
 
+def test_headline_instance_keeps_three_waves(gpu):
+    """The planner's headline depth on wide B3/S23 tori (G = 10, the
+    row-pair-shared circuit) holds 3 waves per SIMD
+    (12 per CU): at 163 VGPRs it sits 5 below the 3-wave limit, and a change
+    that crosses it (G = 11 / 12 already run at 2) must show here rather than
+    only as a slower bench."""
+    with engine(262144, 64) as e:
+        assert e.pass_plan(20) == [10, 10]
+        assert e.occupancy(10)[0] >= 12
+        assert e.occupancy(8)[0] >= 12
+
+
 @pytest.mark.parametrize("gpp", DEPTHS)
 @pytest.mark.parametrize("words", WORDS)
 def test_unhashed_every_depth(gpu, words, gpp):
