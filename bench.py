@@ -435,6 +435,8 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
          "valu": {"instructions_per_word_generation": {k: n for k, (n, _) in mix.items()},
                   "cycles_per_word_generation": round(cycles, 2),
                   "measured_valu_per_word_generation": round(pmc["valu_per_word_gen"], 2) if pmc else None,
+                  "circuit": ("per-row full-sum B3/S23 (rule_b3s23_fullsum), quad layout" if quads else
+                              "row-pair-shared B3/S23 (pair_sum + rule_b3s23_pair)"),
                   "source": "loop census scripts/isa_loop.py; issue costs profiles/r01_valu_op_costs.txt"},
          **common}
     held = {"clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None}
