@@ -310,12 +310,14 @@ __device__ __forceinline__ uint32_t rule_b3s23_fullsum(uint32_t a0, uint32_t a1,
 // m + 1 (m even) both sum h(m) + h(m + 1); their binary sum P (0..6, three
 // planes) is formed once and each row adds its own third h:
 //   S(m) = h(m - 1) + P,  S(m + 1) = P + h(m + 2).
-// The 4-gate tail takes P, the third row's (x1 x0) and the centre; it was
-// found by exhaustive search over 4-gate 3-input circuits on the binary P
-// (DESIGN.md §4 "Rule circuit"; none of 3 gates exists for any 3-plane code of
-// P, and no 3-gate sum of a + b separates its values), and is checked on
-// every input by tests/test_rule_circuit.py.  Per two rows: 4 + 2 x 4 gates
-// instead of 2 x 7.
+// The 4-gate tail takes P, the third row's (x1 x0) and the centre; both
+// rows' centres lie inside P's two rows, so P = 0 with a live centre never
+// occurs and the tail may treat it as a don't-care.  It was found by
+// exhaustive search over 4-gate 3-input circuits on the binary P (DESIGN.md
+// section 4 "Row-pair-shared circuit", scripts/circuit_search/: no 3-gate
+// tail exists for any 3-plane code of P, and no 3 gates over a + b separate
+// its values) and is checked on every input by tests/test_rule_circuit.py.
+// Per two rows: 4 + 2 x 4 gates instead of 2 x 7.
 constexpr uint32_t kPairT1 = 0x43;
 constexpr uint32_t kPairT2 = 0x18;
 constexpr uint32_t kPairT3 = 0x26;
