@@ -105,7 +105,8 @@ class Job:
     Ranks come from the launcher's environment (torch.distributed.run sets
     RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Rank 0's RCCL
     unique id reaches the other ranks through a file named after
-    MASTER_ADDR:MASTER_PORT (one node); a file older than this rank's start
+    MASTER_ADDR:MASTER_PORT (one node; under torch.distributed.run also
+    after the elastic agent, the ranks' common parent); a file older than this rank's start
     (minus two minutes of launch skew) is a leftover of an earlier job and is
     ignored.  After the first barrier over the new communicator every rank
     has read it, and rank 0 removes it.  Barriers and the
@@ -122,8 +123,13 @@ class Job:
         self.t_start = time.time()
 
     def uid_path(self):
+        # Under torch.distributed.run every local rank is a child of the same
+        # elastic agent, so the agent's pid tells this job's file from one a
+        # crashed earlier job on the same port left behind (its run id is
+        # "none" unless --rdzv-id is given).  Other launchers: address + port.
+        agent = str(os.getppid()) if "TORCHELASTIC_RUN_ID" in os.environ else ""
         key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
-                        os.environ.get("TORCHELASTIC_RUN_ID", "")])
+                        os.environ.get("TORCHELASTIC_RUN_ID", ""), agent])
         return os.path.join(tempfile.gettempdir(), "gol_bench_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16])
 
     def join(self, eng, N, timeout=300.0):

@@ -82,3 +82,16 @@ def test_gather_lays_rows_by_rank(monkeypatch):
 
     job.eng = Sum()
     assert job.gather([1, 2, 3]) == [[7, 8, 9], [1, 2, 3]]
+
+
+def test_torchrun_key_names_the_agent(monkeypatch):
+    """Under torch.distributed.run (TORCHELASTIC_RUN_ID set) the file name
+    also carries the ranks' common parent, the elastic agent: a file a
+    crashed earlier torchrun job on the same port left is never read."""
+    job = _job(monkeypatch, 1, 41010)
+    plain = job.uid_path()
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    here = job.uid_path()
+    monkeypatch.setattr(os, "getppid", lambda: 1)
+    other_agent = job.uid_path()
+    assert len({plain, here, other_agent}) == 3
