@@ -151,3 +151,23 @@ def test_single_rank_ring_windows_carry_parity(tmp_path):
     boards = {c["board"] for c in d["parity"]["checks"]}
     assert boards == {"65536x65536", "262144x262144", "262144x32768"}
     assert d["parity"]["match"] is True
+
+
+def test_torchrun_launch_like_the_driver(tmp_path):
+    """The driver's own launch form: python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
+    bench.py ... (here the fake runner): the ranks find each other through
+    the rendezvous file keyed by the elastic agent, and rank 0 prints the
+    one line."""
+    port = _free_port()
+    env = dict(os.environ, FAKE_LOG_DIR=str(tmp_path), OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), RUNNER,
+                        "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu"],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["parity"]["match"] is True
+    assert sum(d["ranks"]["rows"]) == 262144
