@@ -69,7 +69,7 @@ struct gol_ctx {
     int32_t topology = GOL_TORUS;
     uint32_t birth = 0, survive = 0;
     int64_t vis_w = 0, vis_h = 0;
-    int ilv = 1;         // device words per interleave group: 1 row-major, 2 pairs, 4 quads
+    int ilv = 1;         // device words per interleave group: 1 row-major, 2 pairs
     int device = 0;
     int vec_fixed = 0;  // words per lane forced by gol_set_tuning (0: per-pass automatic)
     // device state
@@ -219,12 +219,6 @@ bool life_torus(const gol_ctx* c) {
     return c->topology == GOL_TORUS && c->birth == GOL_RULE_LIFE_BIRTH && c->survive == GOL_RULE_LIFE_SURVIVE;
 }
 
-// Deepest pass of the 16-byte-lane generic-rule and clipped kernel instances
-// that keeps every variable in registers: deeper ones spill (448-640 B of
-// scratch per lane from G = 8, hashed clipped, on; every one of them at
-// G >= 10; `make asm` resource usage).
-constexpr int kMaxGensVec4Generic = 7;
-
 int bind(gol_ctx* ctx) {
     HIP_CHECK(ctx, hipSetDevice(ctx->device));
     return GOL_OK;
@@ -355,40 +349,17 @@ EventPair* next_event_pair(gol_ctx* ctx) {
 // Device layout of a board: words per interleave
 // group.  Tori keep their columns interleaved so the stencil needs fewer
 // funnel shifts: pairs (one v_alignbit and one DPP move per word and
-// generation) where a row holds whole pairs; clipped boards stay row-major
-// (any width).  GOL_LAYOUT=quads makes tori that hold whole quads
-// quad-interleaved (one of each per two words, 16-byte lanes at 2 waves per
-// SIMD): the round-4 experiment, slower than pairs on MI355X (DESIGN.md
-// section 4 "Quad layout"), kept as an opt-in, tested layout.  The state
-// hash is defined over the device words, so the oracle follows the same
-// switch (oracle_device_ilv) and the golden tables hold pair-layout hashes.
-bool quads_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("GOL_LAYOUT");
-        return e && strcmp(e, "quads") == 0;
-    }();
-    return on;
-}
-
+// generation) where a row holds whole pairs; every other board stays
+// row-major (any width).  A function of the geometry alone -- no setting or
+// environment variable changes it -- and invisible at the boundary: host
+// buffers are row-major and the state hash reads the cells through canonical
+// words (section 5), so the same board hashes alike in either layout.
 int device_ilv(int32_t topology, int64_t wwords) {
     if (topology != GOL_TORUS) return 1;
-    if (wwords % 4 == 0 && quads_enabled()) return 4;
     return wwords % 2 == 0 ? 2 : 1;
 }
 
-// Multi-generation kernel formulation (gol_stencil.h): 1 = vertical-first,
-// 2 = horizontal-first (default: ~13.5 instead of ~15.4 VALU per word and
-// generation; +9 % at 262144^2, +24 % at 65536^2, profiles/r01_variant_ab.txt).
-// GOL_STENCIL_VARIANT overrides (A/B experiments).
 constexpr int kDefaultXcdChunk = 8;
-
-int stencil_variant() {
-    static const int v = [] {
-        const char* e = getenv("GOL_STENCIL_VARIANT");
-        return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 2;
-    }();
-    return v;
-}
 
 // Blocks per XCD chunk of the step kernels' block order (gol_stencil.h
 // xcd_block).  GOL_XCD_CHUNK overrides (A/B experiments; 1 = dispatch order).
@@ -416,15 +387,6 @@ int xcd_chunk(int gens, int strips) {
     return std::min(64, std::max(kDefaultXcdChunk, 4 * blocks_per_band));
 }
 
-// Kernel formulation a pass of `gens` generations at `vec` words per lane
-// actually runs: 16-byte lanes use the vertical-first kernel, except B3/S23
-// on the quad layout up to gol::kMaxGensQuadHg generations per pass (deeper
-// rings spill; gol_stencil.h kHgLanes).
-int kernel_variant(const gol_ctx* ctx, int vec, bool life, int gens) {
-    if (vec == 4) return (ctx->ilv == 4 && life && gens <= gol::kMaxGensQuadHg) ? stencil_variant() : 1;
-    return stencil_variant();
-}
-
 // Words per lane for a single-generation pass: 16-byte lane loads where the
 // row fills whole waves of them.
 int default_vec(int64_t wwords) {
@@ -435,23 +397,16 @@ int default_vec(int64_t wwords) {
 // carry 62 output lanes, so a row of w words needs ceil(w / (62 v)) strips;
 // prefer 16-byte lanes unless 8-byte lanes waste clearly fewer lanes.
 int lane_words(const gol_ctx* ctx, int gens) {
-    // an interleaved layout needs whole groups per lane: pairs 8- or 16-byte
-    // lanes, quads 16-byte lanes
+    // the pair layout needs whole pairs per lane: 8- or 16-byte lanes
     if (ctx->vec_fixed > 0) return std::max(ctx->vec_fixed, ctx->ilv);
     const int64_t w = ctx->wwords;
-    if (ctx->ilv == 4) return 4;
     if (gens == 1) return ctx->ilv == 2 ? std::max(default_vec(w), 2) : default_vec(w);
-    auto util = [&](int v) -> double {
-        const int64_t strips = (w / v + 61) / 62;
-        return (double)(w / v) / (double)(strips * 64);
-    };
-    const bool ok4 = w % 4 == 0 && w >= 4 * 62, ok2 = w % 2 == 0 && w >= 2 * 62;
     // the horizontal-first kernel keeps 3 planes per ring row: 8-byte lanes
-    // (95 VGPRs at G = 6, 5 waves/SIMD) beat 16-byte lanes (183 VGPRs, 2 waves)
-    if (stencil_variant() == 2) return ok2 || ctx->ilv == 2 ? 2 : 1;
-    if (ok4 && (!ok2 || util(4) >= util(2) - 0.03)) return 4;
-    if (ok2 || ctx->ilv == 2) return 2;
-    return 1;
+    // (95 VGPRs at G = 6, 5 waves/SIMD) beat 16-byte lanes (183 VGPRs, 2 waves;
+    // those run the vertical-first kernel, +9 % at 262144^2 and +24 % at
+    // 65536^2 for 8-byte horizontal-first lanes, profiles/r01_variant_ab.txt)
+    const bool ok2 = w % 2 == 0 && w >= 2 * 62;
+    return ok2 || ctx->ilv == 2 ? 2 : 1;
 }
 
 // `resident`: waves the whole GPU holds at once for this kernel (0: unknown).
@@ -581,12 +536,11 @@ TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int
 
 // Resident waves on the whole GPU for a launch (cached occupancy query).
 int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
-    const int variant = kernel_variant(ctx, vec, life, gens);
-    const int key = (((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 4 +
-                     variant) * 8 + ctx->ilv;
+    const int key = ((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 8 +
+                    ctx->ilv;
     auto it = ctx->occupancy_cache.find(key);
     if (it != ctx->occupancy_cache.end()) return it->second;
-    const int blocks = gol::resident_blocks_per_cu(vec, gens, variant, life, hash, clipped, ctx->ilv);
+    const int blocks = gol::resident_blocks_per_cu(vec, gens, life, hash, clipped, ctx->ilv);
     const int64_t waves = (int64_t)blocks * gol::kWavesPerWG * ctx->num_cus;
     ctx->occupancy_cache[key] = waves;
     return waves;
@@ -660,7 +614,6 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wrap_x = ctx->topology == GOL_TORUS ? 1 : 0;
     p.birth = ctx->birth;
     p.survive = ctx->survive;
-    p.variant = kernel_variant(ctx, vec, life, gens);
     p.xcd_chunk = xcd_chunk(gens, p.strips);
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
@@ -1146,11 +1099,10 @@ int depth_cap(const gol_ctx* ctx) {
     int64_t G = ctx->gens_per_pass > 0 ? ctx->gens_per_pass
                                        : (life_torus(ctx) ? gol::kMaxGensPerPass : kMaxGensPlannedGeneric);
     G = std::min<int64_t>(G, gol::kMaxGensPerPass);
-    // 16-byte lanes (forced by tuning, or implied by the quad layout): the
-    // generic-rule / clipped instances deeper than this spill (gol_set_tuning
-    // refuses them as fixed depths with words_per_lane = 4)
-    if ((ctx->vec_fixed == 4 || ctx->ilv == 4) && !life_torus(ctx))
-        G = std::min<int64_t>(G, kMaxGensVec4Generic);
+    // 16-byte lanes (forced by tuning): the generic-rule / clipped instances
+    // deeper than this spill and are not built (gol_set_tuning refuses them
+    // as fixed depths with words_per_lane = 4)
+    if (ctx->vec_fixed == 4 && !life_torus(ctx)) G = std::min<int64_t>(G, gol::kMaxGensVec4Generic);
     if (in_ring(ctx)) G = std::min<int64_t>(G, ctx->height / ctx->nranks);
     if (ctx->group) G = std::min<int64_t>(G, group_min_rows(ctx->group));
     return (int)std::max<int64_t>(G, 1);
@@ -2008,11 +1960,11 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     if (words_per_lane > 0 && ctx->wwords % words_per_lane != 0)
         return set_err(ctx, GOL_EINVAL, "words_per_lane %d does not divide the %d words of a row", words_per_lane,
                        ctx->wwords);
-    if (words_per_lane == 4 && !life_torus(ctx) && gens_per_pass > kMaxGensVec4Generic)
+    if (words_per_lane == 4 && !life_torus(ctx) && gens_per_pass > gol::kMaxGensVec4Generic)
         return set_err(ctx, GOL_EINVAL,
                        "words_per_lane 4 with gens_per_pass %d > %d: the generic-rule / clipped kernel instance "
-                       "would spill registers to scratch",
-                       gens_per_pass, kMaxGensVec4Generic);
+                       "would spill registers to scratch (not built)",
+                       gens_per_pass, gol::kMaxGensVec4Generic);
     ctx->band_rows = band_rows;
     ctx->gens_per_pass = gens_per_pass;
     ctx->vec_fixed = words_per_lane;
@@ -2038,7 +1990,7 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int vec = lane_words(ctx, gens_per_pass);
     const int blocks =
-        gol::resident_blocks_per_cu(vec, gens_per_pass, kernel_variant(ctx, vec, life, gens_per_pass), life, false, clipped, ctx->ilv);
+        gol::resident_blocks_per_cu(vec, gens_per_pass, life, false, clipped, ctx->ilv);
     if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
     if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
     return GOL_OK;

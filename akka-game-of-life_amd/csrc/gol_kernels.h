@@ -19,15 +19,21 @@ constexpr int kHashSlots = 64;   // sharded hash accumulators (one cache line ea
 constexpr int kHashSlotStride = 8;  // u64 per slot => 64 B apart
 constexpr int kHashGenStride = kHashSlots * kHashSlotStride;  // u64 per generation
 constexpr int kMaxGensPerPass = 12;  // temporal blocking depth supported by the kernels
-constexpr int kMaxGensQuadHg = 8;    // deepest horizontal-first pass on the quad layout (2 waves per SIMD)
+// Deepest pass of the 16-byte-lane (words_per_lane = 4) generic-rule and
+// clipped instances that keeps every variable in registers: deeper ones spill
+// (448-640 B of scratch per lane), so they are not built (gol_stencil.h
+// kBuilt) and gol_set_tuning / the planner never ask for them.
+constexpr int kMaxGensVec4Generic = 7;
 
-// State hash keys (DESIGN.md "State hash"; oracle/gol_oracle.c
-// oracle_hash_packed, oracle/oracle.py np_hash): device word w at global row
-// y, device word column c contributes w * A(y, c % HG) * B(c / HG) mod 2^64,
-// HG = 4 on the quad layout, 2 on every other.
+// State hash keys (oracle/gol_oracle.c
+// oracle_hash_packed, oracle/oracle.py np_hash).  The hash is a function of
+// the cells alone: the canonical words E (even columns) and O (odd columns)
+// of column group g = columns 64g .. 64g + 63 of global row y contribute
+// (E * A(y, 0) + O * A(y, 1)) * B(g) mod 2^64 -- on the pair layout exactly
+// the device words, elsewhere their unzipped row-major words.
 //   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * kHashRowMul (mod 2^32)
-//   A(y, j) = A(y, 0) + j * kHashOddAdd    (even: stays odd)
-//   B(k)    = murmur3 fmix32(k + kHashPairAdd) | 1
+//   A(y, 1) = A(y, 0) + kHashOddAdd        (even: stays odd)
+//   B(g)    = murmur3 fmix32(g + kHashPairAdd) | 1
 // Both keys odd, so a single-word change always changes the sum.
 constexpr uint32_t kHashRowMul = 0x9E3779B1u;
 constexpr uint32_t kHashOddAdd = 0x6A09E666u;
@@ -94,7 +100,6 @@ struct StepParams {
     int64_t halo_stride;       // words between halo rows (0: one row repeated)
     uint32_t birth;
     uint32_t survive;
-    int32_t variant;           // multi-generation kernel: 1 vertical-first, 2 horizontal-first
     int32_t xcd_chunk;         // consecutive blocks kept on one XCD (gol_stencil.h xcd_block; <= 1: off)
     unsigned long long* clk;   // launch clock probe slot (kClockSlotWords u64), or null (gol_stencil.h clock_probe_*)
 };
@@ -111,27 +116,28 @@ int strip_words(int vec, int gens);
 
 // vec: words per lane (1, 2 or 4); gens: generations per pass; life: B3/S23
 // fast path (torus only); hash: fuse the per-generation state hash; clipped:
-// reference geometry; ilv: the plane's interleave (1 row-major, 2 pairs,
-// 4 quads; a multiple of vec).
+// reference geometry; ilv: the plane's interleave (1 row-major, 2 pairs;
+// vec a multiple of it).  Multi-generation passes at vec <= 2 run the
+// horizontal-first kernel, at vec = 4 the vertical-first one.
 hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool hash, bool clipped, int ilv,
                        int grid_x, int grid_y, hipStream_t stream);
 
 // Resident 256-thread workgroups per CU of the step kernel instance a launch
 // with these parameters uses (hipOccupancyMaxActiveBlocksPerMultiprocessor);
 // 0 if unknown.
-int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, int ilv);
+int resident_blocks_per_cu(int vec, int gens, bool life, bool hash, bool clipped, int ilv);
 
 // Seeded board in the device layout (ilv: words per interleave group).
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width,
                        int64_t grow0, int32_t rows, uint64_t seed, int ilv, hipStream_t stream);
 
-// Row-major words <-> interleaved words (ilv 2: pairs, 4: quads), `rows` rows
-// of `wwords` (a multiple of ilv) words, `pitch` words apart in the source
-// and `dst_pitch` (<= 0: `pitch`) in the destination (src != dst).
+// Row-major words <-> pair-interleaved words (ilv 2), `rows` rows of `wwords`
+// (even) words, `pitch` words apart in the source and `dst_pitch` (<= 0:
+// `pitch`) in the destination (src != dst).
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
                           bool to_device, int ilv, hipStream_t stream, int64_t dst_pitch = 0);
 
-// Partial state hash of `rows` device rows (hash group 4 on the quad layout).
+// Partial state hash of `rows` device rows of interleave `ilv` (1 or 2).
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0,
                        int32_t rows, int ilv, unsigned long long* slots, hipStream_t stream);
 

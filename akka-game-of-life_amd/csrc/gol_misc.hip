@@ -16,10 +16,9 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// Interleaved layouts (DESIGN.md "Data layout"; oracle/gol_oracle.c
-// oracle_to_device): pairs -- row-major words (w0, w1) = columns 0..31,
-// 32..63 <-> (e, o) = their even and odd columns; quads -- row-major words
-// w0..w3 = columns 0..127 <-> q0..q3, column 4b + j in bit b of q_j.
+// The pair layout (DESIGN.md "Data layout"; oracle/gol_oracle.c
+// oracle_to_pairs): row-major words (w0, w1) = columns 0..31, 32..63 <->
+// (e, o) = their even and odd columns.
 __device__ __forceinline__ uint32_t even_bits(uint32_t x) {  // bits 0, 2, .., 30 -> 0 .. 15
     x &= 0x55555555u;
     x = (x | (x >> 1)) & 0x33333333u;
@@ -36,40 +35,20 @@ __device__ __forceinline__ uint32_t spread_bits(uint32_t x) {  // bits 0 .. 15 -
     x = (x | (x << 1)) & 0x55555555u;
     return x;
 }
-__device__ __forceinline__ uint32_t fourth_bits(uint32_t x) {  // bits 0, 4, .., 28 -> 0 .. 7
-    x &= 0x11111111u;
-    x = (x | (x >> 3)) & 0x03030303u;
-    x = (x | (x >> 6)) & 0x000F000Fu;
-    x = (x | (x >> 12)) & 0x000000FFu;
-    return x;
-}
-__device__ __forceinline__ uint32_t spread4_bits(uint32_t x) {  // bits 0 .. 7 -> 0, 4, .., 28
-    x &= 0x000000FFu;
-    x = (x | (x << 12)) & 0x000F000Fu;
-    x = (x | (x << 6)) & 0x03030303u;
-    x = (x | (x << 3)) & 0x11111111u;
-    return x;
-}
 
-// Device word j of the interleave group whose row-major words are w[0..ilv).
-__device__ __forceinline__ uint32_t device_word(const uint32_t* w, int ilv, int j) {
-    if (ilv == 4)
-        return fourth_bits(w[0] >> j) | (fourth_bits(w[1] >> j) << 8) | (fourth_bits(w[2] >> j) << 16) |
-               (fourth_bits(w[3] >> j) << 24);
+// Device word j of the pair whose row-major words are w[0..2).
+__device__ __forceinline__ uint32_t device_word(const uint32_t* w, int j) {
     return even_bits(w[0] >> j) | (even_bits(w[1] >> j) << 16);
 }
-// Row-major word i of the interleave group whose device words are q[0..ilv).
-__device__ __forceinline__ uint32_t row_major_word(const uint32_t* q, int ilv, int i) {
-    if (ilv == 4)
-        return spread4_bits(q[0] >> (8 * i)) | (spread4_bits(q[1] >> (8 * i)) << 1) |
-               (spread4_bits(q[2] >> (8 * i)) << 2) | (spread4_bits(q[3] >> (8 * i)) << 3);
+// Row-major word i of the pair whose device words are q[0..2).
+__device__ __forceinline__ uint32_t row_major_word(const uint32_t* q, int i) {
     return spread_bits(q[0] >> (16 * i)) | (spread_bits(q[1] >> (16 * i)) << 1);
 }
 
 // oracle/gol_oracle.c oracle_seed_packed, on device: the seeded stand-in for
 // BoardCreator.scala:23 (Random.nextBoolean() per cell).  On an interleaved
 // layout each thread derives its device word from the row-major words of its
-// group.
+// pair.
 __global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0,
                             int32_t rows, uint64_t seed, int ilv) {
     const int64_t total = (int64_t)rows * wwords;
@@ -82,11 +61,10 @@ __global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int6
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = k / wwords, c = k % wwords;
         uint32_t w;
-        if (ilv > 1) {
-            const int64_t c0 = c - c % ilv;
-            uint32_t g[4] = {0u, 0u, 0u, 0u};
-            for (int i = 0; i < ilv; ++i) g[i] = word(r, c0 + i);
-            w = device_word(g, ilv, (int)(c % ilv));
+        if (ilv == 2) {
+            const int64_t c0 = c - c % 2;
+            const uint32_t g[2] = {word(r, c0), word(r, c0 + 1)};
+            w = device_word(g, (int)(c % 2));
         } else {
             w = word(r, c);
         }
@@ -94,33 +72,41 @@ __global__ void seed_kernel(uint32_t* plane, int64_t pitch, int32_t wwords, int6
     }
 }
 
-// One thread per interleave group (ILV words): row-major <-> device words.
-template <int ILV>
+// One thread per pair: row-major <-> device words.
 __global__ void convert_kernel(const uint32_t* src, uint32_t* dst, int64_t pitch, int64_t dst_pitch, int32_t ngroups,
                                int32_t rows, int to_device) {
     const int64_t total = (int64_t)rows * ngroups;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = k / ngroups, c = ILV * (k % ngroups);
-        uint32_t in[ILV], out[ILV];
+        const int64_t r = k / ngroups, c = 2 * (k % ngroups);
+        const uint32_t in[2] = {src[r * pitch + c], src[r * pitch + c + 1]};
 #pragma unroll
-        for (int i = 0; i < ILV; ++i) in[i] = src[r * pitch + c + i];
-#pragma unroll
-        for (int i = 0; i < ILV; ++i) out[i] = to_device ? device_word(in, ILV, i) : row_major_word(in, ILV, i);
-#pragma unroll
-        for (int i = 0; i < ILV; ++i) dst[r * dst_pitch + c + i] = out[i];
+        for (int i = 0; i < 2; ++i) dst[r * dst_pitch + c + i] = to_device ? device_word(in, i) : row_major_word(in, i);
     }
 }
 
+// The state hash of `rows` rows: pair-layout words are
+// the canonical words; a row-major word c is unzipped into its even and odd
+// columns, the lower (c even) or upper (c odd) halves of its pair's E and O.
 __global__ void hash_kernel(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0, int32_t rows,
-                            int hg, unsigned long long* slots) {
+                            int ilv, unsigned long long* slots) {
     const int64_t total = (int64_t)rows * wwords;
     unsigned long long acc = 0;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total;
          k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = k / wwords, c = k % wwords;
-        const uint32_t a = hash_row_key(grow0 + r) + (uint32_t)(c % hg) * kHashOddAdd;
-        acc += (unsigned long long)plane[r * pitch + c] * ((unsigned long long)a * hash_pair_key((uint32_t)(c / hg)));
+        const uint32_t ae = hash_row_key(grow0 + r), ao = ae + kHashOddAdd;
+        const uint32_t w = plane[r * pitch + c];
+        unsigned long long t;
+        if (ilv == 2) {
+            t = (unsigned long long)w * ((c & 1) ? ao : ae);
+        } else {
+            const uint32_t u = dev::unzip_bits(w);
+            const uint32_t e = (c & 1) ? u << 16 : u & 0xFFFFu;
+            const uint32_t o = (c & 1) ? u & 0xFFFF0000u : u >> 16;
+            t = (unsigned long long)e * ae + (unsigned long long)o * ao;
+        }
+        acc += t * hash_pair_key((uint32_t)(c / 2));
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, kWaveLanes);
@@ -164,27 +150,27 @@ hipError_t launch_step(const StepParams& p, int vec, int gens, bool life, bool h
     }
 }
 
-int resident_blocks_per_cu(int vec, int gens, int variant, bool life, bool hash, bool clipped, int ilv) {
+int resident_blocks_per_cu(int vec, int gens, bool life, bool hash, bool clipped, int ilv) {
     switch (gens) {
-        case 1: return blocks_step_g1(vec, variant, life, hash, clipped, ilv);
-        case 2: return blocks_step_g2(vec, variant, life, hash, clipped, ilv);
-        case 3: return blocks_step_g3(vec, variant, life, hash, clipped, ilv);
-        case 4: return blocks_step_g4(vec, variant, life, hash, clipped, ilv);
-        case 5: return blocks_step_g5(vec, variant, life, hash, clipped, ilv);
-        case 6: return blocks_step_g6(vec, variant, life, hash, clipped, ilv);
-        case 7: return blocks_step_g7(vec, variant, life, hash, clipped, ilv);
-        case 8: return blocks_step_g8(vec, variant, life, hash, clipped, ilv);
-        case 9: return blocks_step_g9(vec, variant, life, hash, clipped, ilv);
-        case 10: return blocks_step_g10(vec, variant, life, hash, clipped, ilv);
-        case 11: return blocks_step_g11(vec, variant, life, hash, clipped, ilv);
-        case 12: return blocks_step_g12(vec, variant, life, hash, clipped, ilv);
+        case 1: return blocks_step_g1(vec, life, hash, clipped, ilv);
+        case 2: return blocks_step_g2(vec, life, hash, clipped, ilv);
+        case 3: return blocks_step_g3(vec, life, hash, clipped, ilv);
+        case 4: return blocks_step_g4(vec, life, hash, clipped, ilv);
+        case 5: return blocks_step_g5(vec, life, hash, clipped, ilv);
+        case 6: return blocks_step_g6(vec, life, hash, clipped, ilv);
+        case 7: return blocks_step_g7(vec, life, hash, clipped, ilv);
+        case 8: return blocks_step_g8(vec, life, hash, clipped, ilv);
+        case 9: return blocks_step_g9(vec, life, hash, clipped, ilv);
+        case 10: return blocks_step_g10(vec, life, hash, clipped, ilv);
+        case 11: return blocks_step_g11(vec, life, hash, clipped, ilv);
+        case 12: return blocks_step_g12(vec, life, hash, clipped, ilv);
         default: return 0;
     }
 }
 
 hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t width, int64_t grow0, int32_t rows,
                        uint64_t seed, int ilv, hipStream_t stream) {
-    if (ilv != 1 && ilv != 2 && ilv != 4) return hipErrorInvalidValue;
+    if (ilv != 1 && ilv != 2) return hipErrorInvalidValue;
     const int64_t total = (int64_t)rows * wwords;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
     return launch_kernel(seed_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, width, grow0, rows, seed,
@@ -194,13 +180,10 @@ hipError_t launch_seed(uint32_t* plane, int64_t pitch, int32_t wwords, int64_t w
 hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int32_t wwords, int32_t rows,
                           bool to_device, int ilv, hipStream_t stream, int64_t dst_pitch) {
     if (dst_pitch <= 0) dst_pitch = pitch;
-    if ((ilv != 2 && ilv != 4) || wwords % ilv != 0) return hipErrorInvalidValue;
-    const int64_t total = (int64_t)rows * (wwords / ilv);
+    if (ilv != 2 || wwords % 2 != 0) return hipErrorInvalidValue;
+    const int64_t total = (int64_t)rows * (wwords / 2);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 8192));
-    if (ilv == 4)
-        return launch_kernel(convert_kernel<4>, dim3(blocks), dim3(256), stream, src, dst, pitch, dst_pitch,
-                             wwords / 4, rows, to_device ? 1 : 0);
-    return launch_kernel(convert_kernel<2>, dim3(blocks), dim3(256), stream, src, dst, pitch, dst_pitch, wwords / 2,
+    return launch_kernel(convert_kernel, dim3(blocks), dim3(256), stream, src, dst, pitch, dst_pitch, wwords / 2,
                          rows, to_device ? 1 : 0);
 }
 
@@ -208,8 +191,9 @@ hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int
                        unsigned long long* slots, hipStream_t stream) {
     const int64_t total = (int64_t)rows * wwords;
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 4096));
-    return launch_kernel(hash_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, grow0, rows,
-                         ilv == 4 ? 4 : 2, slots);
+    if (ilv != 1 && ilv != 2) return hipErrorInvalidValue;
+    return launch_kernel(hash_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, grow0, rows, ilv,
+                         slots);
 }
 
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream) {

@@ -47,20 +47,10 @@ constexpr int kPF = 2;               // step_kernel: rows prefetched ahead
 constexpr int kRing = kPF + 3;       // step_kernel: register ring of stream rows
 constexpr int kMRing = 6;            // multistep kernels: input ring (multiple of 3)
 constexpr int kMPF = 2;              // multistep_kernel: rows prefetched ahead
-#ifndef GOL_HG_PF
-#define GOL_HG_PF 2
-#endif
-#ifndef GOL_HG_PF_QUAD
-#define GOL_HG_PF_QUAD 2
-#endif
-// multistep_hg_kernel: rows prefetched ahead (< kMRing); 16-byte (quad) lanes
-// run at 2 waves per SIMD and may prefetch deeper
-template <int VEC>
-constexpr int kHgPF = VEC == 4 ? GOL_HG_PF_QUAD : GOL_HG_PF;
-static_assert(kHgPF<2> >= 1 && kHgPF<2> < kMRing && kHgPF<4> >= 1 && kHgPF<4> < kMRing, "prefetch slots");
-#ifndef GOL_IDLE_LANES_OFF
-#define GOL_IDLE_LANES_OFF 1        // multistep_hg_kernel: lanes past the last strip's halo lane exit
-#endif
+constexpr int kHgPF = 2;             // multistep_hg_kernel: rows prefetched ahead (< kMRing)
+static_assert(kHgPF >= 1 && kHgPF < kMRing, "prefetch slots");
+static_assert(kMRing % 6 == 0, "the paired-row schedule reads a row's parity from its ring slot (even ring), "
+                                  "the stage rings index slots mod 3");
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
 
@@ -113,43 +103,23 @@ struct Words {
 
 // Unconditional load (callers clamp the column into the row), so no
 // exec-masked branch separates a load from its use and the compiler's
-// counted vmcnt waits keep the prefetch ring in flight.
-#ifndef GOL_NT_LOADS
-#define GOL_NT_LOADS 0
-#endif
-#ifndef GOL_NT_STORES
-#define GOL_NT_STORES 0
-#endif
+// counted vmcnt waits keep the prefetch ring in flight.  Plain (cacheable)
+// loads: the halo rows and edge words are re-read by the neighbouring bands
+// and strips (non-temporal loads measured -13..-20 %).
 template <int VEC>
 __device__ __forceinline__ void load_words(const uint32_t* rp, int col, Words<VEC>& d) {
     if constexpr (VEC == 4) {
-#if GOL_NT_LOADS
-        const U32x4 v = __builtin_nontemporal_load(reinterpret_cast<const U32x4*>(rp + col));
-        d.w[0] = v[0]; d.w[1] = v[1]; d.w[2] = v[2]; d.w[3] = v[3];
-#else
         const uint4 v = *reinterpret_cast<const uint4*>(rp + col);
         d.w[0] = v.x; d.w[1] = v.y; d.w[2] = v.z; d.w[3] = v.w;
-#endif
     } else if constexpr (VEC == 2) {
-#if GOL_NT_LOADS
-        const U32x2 v = __builtin_nontemporal_load(reinterpret_cast<const U32x2*>(rp + col));
-        d.w[0] = v[0]; d.w[1] = v[1];
-#else
         const uint2 v = *reinterpret_cast<const uint2*>(rp + col);
         d.w[0] = v.x; d.w[1] = v.y;
-#endif
     } else {
         d.w[0] = rp[col];
     }
 }
 
 // load_words with the non-temporal hint (NT) or without.
-#ifndef GOL_G1_BAND4
-#define GOL_G1_BAND4 1   // step_kernel: dedicated straight-line path for 4-row bands
-#endif
-#ifndef GOL_G1_NT_MID
-#define GOL_G1_NT_MID 1  // ... whose two middle rows (read by one wave only) load non-temporally
-#endif
 template <int VEC, bool NT>
 __device__ __forceinline__ void load_words_k(const uint32_t* rp, int col, Words<VEC>& d) {
     if constexpr (NT && VEC == 4) {
@@ -171,7 +141,7 @@ __device__ __forceinline__ void load_words_k(const uint32_t* rp, int col, Words<
 // row and the hardware bounds check drops the store.  No exec-mask branch
 // around the store, so the counted vmcnt waits of the loads that follow stay
 // exact (a skippable store makes the compiler wait for the worse path).
-template <int VEC, bool NT = (GOL_NT_STORES != 0)>
+template <int VEC, bool NT = false>
 __device__ __forceinline__ void store_row(uint32_t* row, bool row_ok, int32_t row_bytes, int col, bool lane_ok,
                                           const Words<VEC>& d) {
     const __amdgpu_buffer_rsrc_t rs =
@@ -389,8 +359,8 @@ __device__ __forceinline__ void column_sums(const Words<VEC>& A, const Words<VEC
 // being the previous group's last column) and the last word's east neighbour
 // (the group's first word shifted down, the next group's first column coming
 // in) need a funnel shift.  ILV = 1 is the row-major layout (two shifts per
-// word), ILV = 2 the pair layout (one per word), ILV = 4 the quad layout (one
-// per two words) -- v_alignbit issues at half the rate of v_bitop3 on gfx950.
+// word), ILV = 2 the pair layout (one per word) -- v_alignbit issues at half
+// the rate of v_bitop3 on gfx950.
 template <int ILV, int VEC, typename T>
 __device__ __forceinline__ void neighbours(const T (&v)[VEC], T l, T r, int j, T& w, T& e) {
     // l: the word left of word 0 (the previous lane's last), r: the word right
@@ -452,83 +422,99 @@ __device__ __forceinline__ void rule_words(const StepParams& p, const uint32_t (
     }
 }
 
-// Fused state hash (DESIGN.md "State hash"): device word w at global row y,
-// device word column c contributes w * A(y, c % HG) * B(c / HG) (mod 2^64),
-// HG = 4 on the quad layout and 2 otherwise (kHashGroup), with
-// A(y, j) = A(y, 0) + j kHashOddAdd.  A lane sums w * A over the rows it
-// streams -- one v_mad_u64_u32 per word and generation, the row key A an SGPR
-// computed once per row on the scalar unit -- and multiplies by its column-
-// group key B once, when it flushes (hash_lane_total).  A lane's words share
-// B: one group (VEC = HG, the row's first word index a multiple of HG), two
-// pairs (VEC = 4 on the row-major or pair layouts: two sums), or one word of a
-// pair (VEC = 1: the lane picks the key of its word's parity).
-template <int ILV>
-constexpr int kHashGroup = ILV == 4 ? 4 : 2;
+// Fused state hash, a function of the cells alone: the
+// canonical words E, O of column group g (columns 64g .. 64g + 63: E its even
+// columns, O its odd ones) of global row y contribute
+// (E A(y, 0) + O A(y, 1)) B(g) (mod 2^64), A(y, 1) = A(y, 0) + kHashOddAdd.
+// On the pair layout (ILV = 2) a lane's device words ARE the canonical words,
+// so a lane sums w * A over the rows it streams -- one v_mad_u64_u32 per word
+// and generation, the row key A an SGPR computed once per row on the scalar
+// unit -- and multiplies by its group key B once, when it flushes
+// (hash_lane_total).  Row-major lanes (ILV = 1: clipped boards, tori with an
+// odd word count) unzip each word into its even and odd columns first
+// (unzip_bits) -- the canonical words of the pair the word belongs to.  A
+// lane's words share B per group: VEC = 2 one group, VEC = 4 two (two sums;
+// the row's first word index is even), VEC = 1 half a group (odd_lane: the
+// upper half).
+__device__ __forceinline__ uint32_t unzip_bits(uint32_t x) {
+    // even bits -> 0..15, odd bits -> 16..31 (outer unshuffle, 4 delta swaps)
+    uint32_t t = (x ^ (x >> 1)) & 0x22222222u;
+    x ^= t ^ (t << 1);
+    t = (x ^ (x >> 2)) & 0x0C0C0C0Cu;
+    x ^= t ^ (t << 2);
+    t = (x ^ (x >> 4)) & 0x00F000F0u;
+    x ^= t ^ (t << 4);
+    t = (x ^ (x >> 8)) & 0x0000FF00u;
+    x ^= t ^ (t << 8);
+    return x;
+}
 
-template <int VEC, int HG = 2>
+template <int VEC>
 struct HashAcc {
-    static constexpr int kGroups = VEC >= HG ? VEC / HG : 1;
+    static constexpr int kGroups = VEC >= 2 ? VEC / 2 : 1;
     unsigned long long a[kGroups];
 };
 
-template <int VEC, int HG>
-__device__ __forceinline__ void hash_clear(HashAcc<VEC, HG>& h) {
+template <int VEC>
+__device__ __forceinline__ void hash_clear(HashAcc<VEC>& h) {
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k) h.a[k] = 0;
+    for (int k = 0; k < HashAcc<VEC>::kGroups; ++k) h.a[k] = 0;
 }
 
 // One output row with row keys ae = A(y, 0), ao = A(y, 1) (both 0: the row
-// is not hashed; A(y, 2), A(y, 3) follow as 2 ao - ae, 3 ao - 2 ae); odd_lane:
-// VEC = 1 lanes of odd words.
-template <int VEC, int HG>
+// is not hashed); odd_lane: VEC = 1 lanes holding a group's second word.
+template <int VEC, int ILV>
 __device__ __forceinline__ void hash_row_keys(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
-                                              HashAcc<VEC, HG>& h) {
-    if constexpr (VEC == 1) {
-        static_assert(HG == 2, "a quad spans four words");
-        h.a[0] += (unsigned long long)o.w[0] * (unsigned long long)(odd_lane ? ao : ae);
-    } else {
-        static_assert(VEC % HG == 0, "whole hash groups per lane");
+                                              HashAcc<VEC>& h) {
+    if constexpr (ILV == 2) {
+        static_assert(VEC % 2 == 0, "whole pairs per lane");
 #pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            const int ph = j % HG;
-            const uint32_t key = ph == 0 ? ae : ph == 1 ? ao : (uint32_t)ph * ao - (uint32_t)(ph - 1) * ae;
-            h.a[j / HG] += (unsigned long long)o.w[j] * (unsigned long long)key;
+        for (int j = 0; j < VEC; ++j)
+            h.a[j / 2] += (unsigned long long)o.w[j] * (unsigned long long)((j & 1) ? ao : ae);
+    } else if constexpr (VEC == 1) {
+        const uint32_t u = unzip_bits(o.w[0]);
+        const uint32_t e = odd_lane ? u << 16 : u & 0xFFFFu;
+        const uint32_t d = odd_lane ? u & 0xFFFF0000u : u >> 16;
+        h.a[0] += (unsigned long long)e * ae + (unsigned long long)d * ao;
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; j += 2) {
+            const uint32_t u0 = unzip_bits(o.w[j]), u1 = unzip_bits(o.w[j + 1]);
+            const uint32_t e = (u0 & 0xFFFFu) | (u1 << 16), d = (u0 >> 16) | (u1 & 0xFFFF0000u);
+            h.a[j / 2] += (unsigned long long)e * ae + (unsigned long long)d * ao;
         }
     }
 }
 
 // One output row at global row `grow`.
-template <int VEC, int HG>
-__device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool odd_lane, HashAcc<VEC, HG>& h) {
+template <int VEC, int ILV>
+__device__ __forceinline__ void hash_row(int64_t grow, const Words<VEC>& o, bool odd_lane, HashAcc<VEC>& h) {
     const uint32_t ae = hash_row_key(grow);
-    hash_row_keys<VEC, HG>(ae, ae + kHashOddAdd, o, odd_lane, h);
+    hash_row_keys<VEC, ILV>(ae, ae + kHashOddAdd, o, odd_lane, h);
 }
 
 // The horizontal-first kernel keeps its per-generation sums in LDS, one u64
 // per lane, pair and generation, added to with ds_add_u64 (no return): 2G
 // fewer VGPRs than register sums, which at G = 6..8 is a wave per SIMD.
-#ifndef GOL_HASH_LDS
-#define GOL_HASH_LDS 1
-#endif
-template <int VEC, int HG>
+template <int VEC, int ILV>
 __device__ __forceinline__ void hash_row_lds(uint32_t ae, uint32_t ao, const Words<VEC>& o, bool odd_lane,
                                              unsigned long long* slot) {
-    HashAcc<VEC, HG> t;
+    HashAcc<VEC> t;
     hash_clear(t);
-    hash_row_keys<VEC, HG>(ae, ao, o, odd_lane, t);
+    hash_row_keys<VEC, ILV>(ae, ao, o, odd_lane, t);
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k) atomicAdd(slot + k * kWaveLanes, t.a[k]);
+    for (int k = 0; k < HashAcc<VEC>::kGroups; ++k) atomicAdd(slot + k * kWaveLanes, t.a[k]);
 }
 
 // The lane's contribution: its sums times their column-group keys (words
-// col .. col + VEC - 1; col a multiple of HG when VEC >= HG), or 0 for a lane
-// that owns no words.
-template <int VEC, int HG>
-__device__ __forceinline__ unsigned long long hash_lane_total(const HashAcc<VEC, HG>& h, int col, bool owns) {
+// col .. col + VEC - 1; col even when VEC >= 2), or 0 for a lane that owns no
+// words.
+template <int VEC>
+__device__ __forceinline__ unsigned long long hash_lane_total(const HashAcc<VEC>& h, int col, bool owns) {
     unsigned long long t = 0;
 #pragma unroll
-    for (int k = 0; k < HashAcc<VEC, HG>::kGroups; ++k)
-        t += h.a[k] * (unsigned long long)hash_pair_key((uint32_t)(col / HG) + (uint32_t)k);
+    for (int k = 0; k < HashAcc<VEC>::kGroups; ++k)
+        t += h.a[k] * (unsigned long long)hash_pair_key((uint32_t)(col / 2) + (uint32_t)k);
     return owns ? t : 0ull;
 }
 
@@ -559,14 +545,10 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
 // 262144^2 3.129 -> 3.003 ms, 262144 x 32768 0.399 -> 0.383 ms per
 // generation.  The multi-generation kernels keep plain stores (round 1:
 // -3..-8 % at G = 6 with non-temporal stores, profiles/r01_bandwidth.txt).
-#ifndef GOL_G1_NT_STORES
-#define GOL_G1_NT_STORES 1
-#endif
-constexpr bool kG1NtStores = GOL_NT_STORES || GOL_G1_NT_STORES;
+constexpr bool kG1NtStores = true;
 
 template <int VEC, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const StepParams p) {
-    constexpr int HG = kHashGroup<ILV>;
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
@@ -575,7 +557,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
     unsigned long long acc = 0;
 
     if (bandi < p.nbands[rg]) {
-        HashAcc<VEC, HG> hacc;
+        HashAcc<VEC> hacc;
         hash_clear(hacc);
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
         const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
@@ -659,7 +641,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             const int r = out_of(i);
             store_row<VEC, kG1NtStores>(p.nxt + (int64_t)r * p.pitch, in_band, p.wwords * 4, col, active, o);
             if constexpr (HASH) {
-                if (in_band) hash_row<VEC, HG>(p.grow0 + r, o, odd_lane, hacc);
+                if (in_band) hash_row<VEC, ILV>(p.grow0 + r, o, odd_lane, hacc);
             }
         };
         auto step_i = [&](int i, int u, bool in_band) {
@@ -667,13 +649,12 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             step_rows(i, ring[ua], ring[uc], ring[ub], edge[ua], edge[uc], edge[ub], in_band);
         };
 
-#if GOL_G1_BAND4
         // The single-generation pass's own band heights (pick_band): the B + 2
         // stream rows issued at once, each once, and B steps.  The B - 2
         // middle rows are read by this wave alone -- the two edge rows and
         // the two halo rows are also a neighbouring band's halo or edge rows,
         // kept in the caches for that second reader -- so they load
-        // non-temporally (GOL_G1_NT_MID).
+        // non-temporally.
         auto band_path = [&](auto BB) __attribute__((always_inline)) {
             constexpr int B = decltype(BB)::value;
             Words<VEC> rs[B + 2];
@@ -681,7 +662,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             static_for<B + 2>([&](auto T) __attribute__((always_inline)) {
                 constexpr int t = decltype(T)::value;
                 const uint32_t* rp = row_ptr(p, row_of(t), 1);
-                load_words_k<VEC, GOL_G1_NT_MID != 0 && t >= 2 && t <= B - 1>(rp, lcolumn, rs[t]);
+                load_words_k<VEC, (t >= 2 && t <= B - 1)>(rp, lcolumn, rs[t]);
                 es[t] = rp[ecol];
             });
             static_for<B>([&](auto I) __attribute__((always_inline)) {
@@ -695,9 +676,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
             band_path(std::integral_constant<int, 6>{});
         } else if (nrows == 8) {
             band_path(std::integral_constant<int, 8>{});
-        } else
-#endif
-        {
+        } else {
             // Loads are never predicated: stream rows past the band's last one
             // are clamped to it, and steps past the band compute into the void
             // (their stores are skipped), so the loop body is straight-line.
@@ -725,7 +704,6 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void step_kernel(const Ste
 // --------------------------------------------------------------------------
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(const StepParams p) {
-    constexpr int HG = kHashGroup<ILV>;
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
     constexpr int kOut = (kWaveLanes - 2) * VEC;  // output words per strip
@@ -764,7 +742,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
         }
         const bool odd_lane = (col & 1) != 0;
-        HashAcc<VEC, HG> hacc[G];
+        HashAcc<VEC> hacc[G];
 #pragma unroll
         for (int s = 0; s < G; ++s) hash_clear(hacc[s]);
         const bool up = (bandi & 1) != 0;
@@ -817,7 +795,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                 if (s < G) {
                     st[s - 1][((u - s) % 3 + 3) % 3] = o;
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, HG>(p.grow0 + brow(m), o, odd_lane, hacc[s - 1]);
+                        if (own_row) hash_row<VEC, ILV>(p.grow0 + brow(m), o, odd_lane, hacc[s - 1]);
                     }
                     // stage s+1: stream row q-s-1 from stage-s rows q-s-2, q-s-1, q-s
                     apply(st[s - 1][((u - s - 2) % 3 + 3) % 3], st[s - 1][((u - s - 1) % 3 + 3) % 3],
@@ -826,7 +804,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
                     if constexpr (HASH) {
-                        if (own_row) hash_row<VEC, HG>(p.grow0 + r, o, odd_lane, hacc[G - 1]);
+                        if (own_row) hash_row<VEC, ILV>(p.grow0 + r, o, odd_lane, hacc[G - 1]);
                     }
                 }
             }
@@ -935,44 +913,15 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
     }
 }
 
-// Minimum waves per SIMD the register allocator must fit: the hashed B3/S23
-// 8-generation instance lands 4 VGPRs over the 4-wave limit (128) without it
-// (with it: 4 dwords spilled).  -DGOL_HG_MINWAVES8=1 builds the unforced
-// variant for A/B runs (scripts/ab_build.sh).
-#ifndef GOL_HG_MINWAVES8
-#define GOL_HG_MINWAVES8 4
-#endif
-#ifndef GOL_HG_MINWAVES_DEEP
-#define GOL_HG_MINWAVES_DEEP 3
-#endif
-// Quad-layout lanes (VEC = 4): two waves per SIMD, 256 VGPRs.
-#ifndef GOL_HG_MINWAVES_QUAD
-#define GOL_HG_MINWAVES_QUAD 2
-#endif
 // The horizontal-first B3/S23 torus kernels share each even/odd row pair's
-// middle sum (rule_b3s23_pair); -DGOL_PAIR_ROWS=0 builds the per-row circuit.
-#ifndef GOL_PAIR_ROWS
-#define GOL_PAIR_ROWS 1
-#endif
-// Quad lanes (VEC = 4) keep the per-row circuit: the paired 8-generation
-// instance spills at 256 VGPRs.
+// middle sum (rule_b3s23_pair).  They run at the occupancy their registers
+// give (G <= 10: 3 or more waves per SIMD); forced to more they spill.
 template <int VEC, bool LIFE, bool CLIPPED>
-constexpr bool kPairRows = GOL_PAIR_ROWS && LIFE && !CLIPPED && VEC <= 2;
-
-// The row-pair-shared instances (kPairRows) run at the occupancy their
-// registers give (G <= 10: 3 or more waves per SIMD): forced to the limits
-// above they spill (8 generations hashed: 40 bytes per lane).
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED>
-constexpr int kHgMinWaves = (VEC == 4) ? GOL_HG_MINWAVES_QUAD
-                             : kPairRows<VEC, LIFE, CLIPPED> ? 1
-                             : (VEC == 2 && G == 8 && LIFE && HASH) ? GOL_HG_MINWAVES8
-                             : (VEC == 2 && G >= 10 && LIFE && HASH) ? GOL_HG_MINWAVES_DEEP
-                             : 1;
+constexpr bool kPairRows = LIFE && !CLIPPED && VEC <= 2;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
-__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE, HASH, CLIPPED>)) void multistep_hg_kernel(
-    const StepParams p) {
-    constexpr int HG = kHashGroup<ILV>;
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(const StepParams p) {
+    static_assert(VEC <= 2, "16-byte lanes run the vertical-first kernel");
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
     constexpr int kOut = (kWaveLanes - 2) * VEC;
@@ -984,7 +933,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
     unsigned long long acc[G];
 #pragma unroll
     for (int s = 0; s < G; ++s) acc[s] = 0;
-    __shared__ unsigned long long hash_lds[HASH ? kWavesPerWG * G * HashAcc<VEC, HG>::kGroups * kWaveLanes : 1];
+    __shared__ unsigned long long hash_lds[HASH ? kWavesPerWG * G * HashAcc<VEC>::kGroups * kWaveLanes : 1];
 
     if (bandi < p.nbands[rg]) {
         const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
@@ -995,7 +944,6 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         const int nout = min(kOut, p.wwords - s0);
         const int col = s0 + (lane - 1) * VEC;
         const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
-#if GOL_IDLE_LANES_OFF
         // The last strip of a row owns fewer than 62 lanes' words (4 of 62 pairs
         // at 262144 columns, 32 at 65536): lanes past its right halo lane would
         // only compute garbage.  Switch them off -- an exec-masked lane issues
@@ -1006,7 +954,6 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         if constexpr (!HASH) {
             if (lane > (nout + VEC - 1) / VEC + 1) return;
         }
-#endif
         int lcol;
         bool incol;
         if (p.wrap_x) {
@@ -1024,16 +971,13 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
             omask[j] = CLIPPED ? (incol ? col_mask(p.width, col + j) : 0u) : 0xFFFFFFFFu;
         }
         const bool odd_lane = (col & 1) != 0;
-        constexpr int kNP = HashAcc<VEC, HG>::kGroups;
+        constexpr int kNP = HashAcc<VEC>::kGroups;
         // this lane's LDS sums: generation s, pair k at hsum[(s * kNP + k) * kWaveLanes]
         unsigned long long* hsum = hash_lds + (size_t)wave_in_wg * G * kNP * kWaveLanes + lane;
         if constexpr (HASH) {
 #pragma unroll
             for (int k = 0; k < G * kNP; ++k) hsum[k * kWaveLanes] = 0ull;
         }
-        HashAcc<VEC, HG> hreg[GOL_HASH_LDS ? 1 : G];  // -DGOL_HASH_LDS=0: register sums (A/B builds)
-#pragma unroll
-        for (int s = 0; s < (GOL_HASH_LDS ? 1 : G); ++s) hash_clear(hreg[s]);
         const bool up = (bandi & 1) != 0;
         auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
         auto vis = [&](int m) -> bool { return row_visible<CLIPPED>(p, brow(m)); };
@@ -1069,14 +1013,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 #pragma unroll
         for (int k = 0; k <= G; ++k) kae[k] = kao[k] = 0u;
 
-        // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF<VEC>,
+        // Stream row q (ring slot u = q % kMRing): prefetch row q + kHgPF,
         // input row q arrives at ring 0, stage s produces stream row q - s.
         // Stage s has valid inputs only from q = 2s on (its rows m < s are
         // built from the clamped rows before the band and are never stored,
         // hashed or read by a valid row), so the pipeline fill -- the first
         // kFill rows, q known at compile time -- skips those stage steps.
         auto row_step = [&](const int q, const int u, const bool fill) __attribute__((always_inline)) {
-            load_m(min(q + kHgPF<VEC>, n_in - 1), in[(u + kHgPF<VEC>) % kMRing]);
+            load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
             if constexpr (HASH) {
 #pragma unroll
                 for (int k = G; k >= 1; --k) {
@@ -1119,11 +1063,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
                 }
                 const bool own_row = m >= G && m < n_in - G;
                 if constexpr (HASH) {
-#if GOL_HASH_LDS
-                    hash_row_lds<VEC, HG>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
-#else
-                    hash_row_keys<VEC, HG>(kae[s], kao[s], o, odd_lane, hreg[s - 1]);
-#endif
+                    hash_row_lds<VEC, ILV>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
                 }
                 if (s < G) {
                     arrive<VEC, CLIPPED, ILV>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
@@ -1135,19 +1075,14 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         };
 
 #pragma unroll
-        for (int t = 0; t < kHgPF<VEC>; ++t) load_m(min(t, n_in - 1), in[t]);
-#ifndef GOL_HASH_PEEL_MAXG
-#define GOL_HASH_PEEL_MAXG 12
-#endif
+        for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
         constexpr int kFill = (2 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
         // The peeled fill is one long straight-line block; only the B3/S23
         // instances keep their rings in registers through it (the generic-rule
-        // mux tree makes the scheduler spill, and so do the hashed instances
-        // at G >= 10: 1.4 KB of scratch), so they alone skip the dead fill
-        // steps.  Hashed G = 8 peeled: 122 VGPRs, no spill (unpeeled: 128
-        // forced + 4 dwords spilled).
+        // mux tree makes the scheduler spill), so they alone skip the dead
+        // fill steps.
         int q_begin = 0;
-        if constexpr (LIFE && (!HASH || G <= GOL_HASH_PEEL_MAXG)) {
+        if constexpr (LIFE) {
             static_for<kFill>([&](auto Q) __attribute__((always_inline)) { row_step(Q.value, Q.value % kMRing, true); });
             q_begin = kFill;
         }
@@ -1158,11 +1093,10 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
         if constexpr (HASH) {
 #pragma unroll
             for (int s = 0; s < G; ++s) {
-                HashAcc<VEC, HG> h;
+                HashAcc<VEC> h;
 #pragma unroll
                 for (int k = 0; k < kNP; ++k) {
-                    if constexpr (GOL_HASH_LDS) h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
-                    else h.a[k] = hreg[s].a[k];
+                    h.a[k] = hsum[(s * kNP + k) * kWaveLanes];
                 }
                 acc[s] = hash_lane_total(h, col, owns);
             }
@@ -1177,29 +1111,30 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG, (kHgMinWaves<VEC, G, LIFE,
 
 // The horizontal-first kernel keeps three planes per ring row: at 16-byte
 // lanes it needs 183-270 registers or spills (1-1.6 KB scratch per lane), so
-// VEC = 4 runs the vertical-first kernel (kernel_variant()) -- except the
-// B3/S23 quad layout, whose full-sum circuit needs fewer planes and whose
-// interleave halves the shifts: 2 waves per SIMD (kHgMinWaves).
-template <int VEC, int ILV, bool LIFE, int G>
-constexpr bool kHgLanes = VEC <= 2 || (ILV == 4 && LIFE && G <= kMaxGensQuadHg);
+// VEC = 4 (gol_set_tuning's words_per_lane = 4) runs the vertical-first
+// kernel.  Its generic-rule and clipped instances deeper than
+// kMaxGensVec4Generic spill and are neither built nor launched (gol_capi.cpp
+// refuses such a tuning).
+template <int VEC, int G, bool LIFE, bool CLIPPED>
+constexpr bool kBuilt = G == 1 || VEC <= 2 || (LIFE && !CLIPPED) || G <= kMaxGensVec4Generic;
 
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
 hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     const dim3 grid(gx, gy), block(kWaveLanes * kWavesPerWG);
     if constexpr (G == 1) {
         return launch_kernel(step_kernel<VEC, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
+    } else if constexpr (!kBuilt<VEC, G, LIFE, CLIPPED>) {
+        return hipErrorInvalidValue;
+    } else if constexpr (VEC <= 2) {
+        return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     } else {
-        if constexpr (kHgLanes<VEC, ILV, LIFE, G>) {
-            if (p.variant == 2)
-                return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
-        }
         return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     }
 }
 
 // Resident 256-thread workgroups per CU for a kernel instance (occupancy API).
 template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
-int blocks_one(int variant) {
+int blocks_one() {
     auto query = [](auto kernel) {
         int n = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kernel, kWaveLanes * kWavesPerWG, 0) != hipSuccess) {
@@ -1210,32 +1145,26 @@ int blocks_one(int variant) {
     };
     if constexpr (G == 1) {
         return query(step_kernel<VEC, LIFE, HASH, CLIPPED, ILV>);
+    } else if constexpr (!kBuilt<VEC, G, LIFE, CLIPPED>) {
+        return 0;
+    } else if constexpr (VEC <= 2) {
+        return query(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>);
     } else {
-        if constexpr (kHgLanes<VEC, ILV, LIFE, G>) {
-            if (variant == 2) return query(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>);
-        }
         return query(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>);
     }
 }
 
 // The instances a launch can select: clipped boards (generic rule, row-major
-// words), tori (B3/S23 fast path or generic rule) in row-major, pair (even
-// lane widths) or quad layout (4-word lanes).  `F` is called with the
-// instance's template arguments as std::integral_constant values.
+// words), tori (B3/S23 fast path or generic rule) in row-major or pair layout
+// (even lane widths).  `F` is called with the instance's template arguments
+// as std::integral_constant values.
 template <int VEC, typename F>
 auto dispatch_kind(bool life, bool hash, bool clipped, int ilv, F&& f) {
     using T = std::true_type;
     using N = std::false_type;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
-    using I4 = std::integral_constant<int, 4>;
     if (clipped) return hash ? f(N{}, T{}, T{}, I1{}) : f(N{}, N{}, T{}, I1{});
-    if constexpr (VEC % 4 == 0) {
-        if (ilv == 4) {
-            if (life) return hash ? f(T{}, T{}, N{}, I4{}) : f(T{}, N{}, N{}, I4{});
-            return hash ? f(N{}, T{}, N{}, I4{}) : f(N{}, N{}, N{}, I4{});
-        }
-    }
     if constexpr (VEC % 2 == 0) {
         if (ilv == 2) {
             if (life) return hash ? f(T{}, T{}, N{}, I2{}) : f(T{}, N{}, N{}, I2{});
@@ -1247,20 +1176,19 @@ auto dispatch_kind(bool life, bool hash, bool clipped, int ilv, F&& f) {
 }
 
 template <int VEC, int G>
-int blocks_variant(int variant, bool life, bool hash, bool clipped, int ilv) {
+int blocks_variant(bool life, bool hash, bool clipped, int ilv) {
     if (VEC % ilv != 0) return 0;
     return dispatch_kind<VEC>(life, hash, clipped, ilv, [&](auto L, auto H, auto C, auto I) {
-        return blocks_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(I)::value>(
-            variant);
+        return blocks_one<VEC, G, decltype(L)::value, decltype(H)::value, decltype(C)::value, decltype(I)::value>();
     });
 }
 
 template <int G>
-int blocks_gens(int vec, int variant, bool life, bool hash, bool clipped, int ilv) {
+int blocks_gens(int vec, bool life, bool hash, bool clipped, int ilv) {
     switch (vec) {
-        case 4: return blocks_variant<4, G>(variant, life, hash, clipped, ilv);
-        case 2: return blocks_variant<2, G>(variant, life, hash, clipped, ilv);
-        default: return blocks_variant<1, G>(variant, life, hash, clipped, ilv);
+        case 4: return blocks_variant<4, G>(life, hash, clipped, ilv);
+        case 2: return blocks_variant<2, G>(life, hash, clipped, ilv);
+        default: return blocks_variant<1, G>(life, hash, clipped, ilv);
     }
 }
 
@@ -1300,17 +1228,17 @@ hipError_t launch_step_g9(const StepParams&, int, bool, bool, bool, int, int, in
 hipError_t launch_step_g10(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
 hipError_t launch_step_g11(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
 hipError_t launch_step_g12(const StepParams&, int, bool, bool, bool, int, int, int, hipStream_t);
-int blocks_step_g1(int, int, bool, bool, bool, int);
-int blocks_step_g2(int, int, bool, bool, bool, int);
-int blocks_step_g3(int, int, bool, bool, bool, int);
-int blocks_step_g4(int, int, bool, bool, bool, int);
-int blocks_step_g5(int, int, bool, bool, bool, int);
-int blocks_step_g6(int, int, bool, bool, bool, int);
-int blocks_step_g7(int, int, bool, bool, bool, int);
-int blocks_step_g8(int, int, bool, bool, bool, int);
-int blocks_step_g9(int, int, bool, bool, bool, int);
-int blocks_step_g10(int, int, bool, bool, bool, int);
-int blocks_step_g11(int, int, bool, bool, bool, int);
-int blocks_step_g12(int, int, bool, bool, bool, int);
+int blocks_step_g1(int, bool, bool, bool, int);
+int blocks_step_g2(int, bool, bool, bool, int);
+int blocks_step_g3(int, bool, bool, bool, int);
+int blocks_step_g4(int, bool, bool, bool, int);
+int blocks_step_g5(int, bool, bool, bool, int);
+int blocks_step_g6(int, bool, bool, bool, int);
+int blocks_step_g7(int, bool, bool, bool, int);
+int blocks_step_g8(int, bool, bool, bool, int);
+int blocks_step_g9(int, bool, bool, bool, int);
+int blocks_step_g10(int, bool, bool, bool, int);
+int blocks_step_g11(int, bool, bool, bool, int);
+int blocks_step_g12(int, bool, bool, bool, int);
 
 }  // namespace gol

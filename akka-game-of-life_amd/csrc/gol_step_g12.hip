@@ -9,8 +9,8 @@ hipError_t launch_step_g12(const StepParams& p, int vec, bool life, bool hash, b
     return dev::launch_gens<12>(p, vec, life, hash, clipped, ilv, gx, gy, st);
 }
 
-int blocks_step_g12(int vec, int variant, bool life, bool hash, bool clipped, int ilv) {
-    return dev::blocks_gens<12>(vec, variant, life, hash, clipped, ilv);
+int blocks_step_g12(int vec, bool life, bool hash, bool clipped, int ilv) {
+    return dev::blocks_gens<12>(vec, life, hash, clipped, ilv);
 }
 
 }  // namespace gol

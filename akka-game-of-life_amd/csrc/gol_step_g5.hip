@@ -9,8 +9,8 @@ hipError_t launch_step_g5(const StepParams& p, int vec, bool life, bool hash, bo
     return dev::launch_gens<5>(p, vec, life, hash, clipped, ilv, gx, gy, st);
 }
 
-int blocks_step_g5(int vec, int variant, bool life, bool hash, bool clipped, int ilv) {
-    return dev::blocks_gens<5>(vec, variant, life, hash, clipped, ilv);
+int blocks_step_g5(int vec, bool life, bool hash, bool clipped, int ilv) {
+    return dev::blocks_gens<5>(vec, life, hash, clipped, ilv);
 }
 
 }  // namespace gol

@@ -185,15 +185,13 @@ def device_count() -> int:
 
 def device_ilv(width: int, topology: int = GOL_TORUS) -> int:
     """Words per interleave group of libgol's device layout (gol_capi.cpp
-    device_ilv): a torus whose rows hold whole pairs of 32-bit words is
-    pair-interleaved (2) -- quad-interleaved (4) when they hold whole quads
-    and GOL_LAYOUT=quads (the opt-in layout) -- any other board row-major (1);
-    the state hash is defined over those device words."""
+    device_ilv, a function of the geometry alone): a torus whose rows hold
+    whole pairs of 32-bit words is pair-interleaved (2), any other board
+    row-major (1).  Informational: host buffers are row-major and the state
+    hash is defined over the cells."""
     ww = (width + 31) // 32
     if topology != GOL_TORUS:
         return 1
-    if ww % 4 == 0 and os.environ.get("GOL_LAYOUT") == "quads":
-        return 4
     return 2 if ww % 2 == 0 else 1
 
 

@@ -72,13 +72,8 @@ DEFAULT_GPP = 0  # generations per HBM pass: 0 = libgol's pass planner (gol_pass
 # 0.47 v_xor + 0.47 v_and per v_alignbit, the (G + 1) / G arrivals included).
 VALU_MIX = {"v_bitop3_b32": (7, 2.3), "v_xor_b32": (0.5, 2.3), "v_and_b32": (0.5, 2.3),
             "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
-# The quad layout (4 interleaved words per lane) keeps the
-# per-row 9-bitop3 circuit; one funnel shift and one DPP move per quad edge,
-# i.e. half of each per word.
-VALU_MIX_QUAD = {"v_bitop3_b32": (9, 2.3), "v_alignbit_b32": (0.5, 4.1), "v_mov_b32_dpp": (0.5, 4.3)}
 # The fused hash adds one v_mad_u64_u32 per word and generation (DESIGN.md "State hash").
 VALU_MIX_HASH = dict(VALU_MIX, v_mad_u64_u32=(1, 4.6))
-VALU_MIX_QUAD_HASH = dict(VALU_MIX_QUAD, v_mad_u64_u32=(1, 4.6))
 
 
 def parse():
@@ -96,6 +91,8 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the N = 1 ring-schedule measurements")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--allow-unchecked", action="store_true",
+                    help="exit 0 when a window has no golden value (boards without a table); a mismatch still fails")
     return ap.parse_args()
 
 
@@ -288,6 +285,12 @@ class Parity:
         self.checks.append(c)
         return c
 
+    def failed(self, allow_unchecked=False):
+        """The checks that did not match (or, unless allow_unchecked, that had
+        no golden value): short labels for the line's closing parity_failed."""
+        return [f'{c["what"]} [{c["board"]}]: ' + ("mismatch" if c["match"] is False else "no golden value")
+                for c in self.checks if c["match"] is False or (c["match"] is None and not allow_unchecked)]
+
     def report(self):
         ms = [c["match"] for c in self.checks]
         used = sorted(golden_path(*k) for k, v in self.tables.items() if v is not None)
@@ -405,11 +408,10 @@ def compact_plan(plan):
     return " + ".join(f"{n} x {g}" for n, g in runs)
 
 
-def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None, quads=False):
+def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False, clock=None):
     """Roofline of the dominant kernel (see the module docstring).  `clock`:
     GHz the timed launches held, from the in-kernel probe (gol_profile_clock):
-    it prices the held_clock diagnostic, never the primary frac.  `quads`:
-    the board is quad-interleaved (the loop's mix has half the shifts)."""
+    it prices the held_clock diagnostic, never the primary frac."""
     if not launches:
         return None
     avg_s = kms / 1e3 / launches
@@ -429,7 +431,7 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
             r["measured_hbm_frac"] = round(pmc["hbm_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS, 4)
             r["traffic_source"] = "profiles/pmc_launch.json " + ", ".join(pmc["keys"])
         return r
-    mix = (VALU_MIX_QUAD_HASH if hashed else VALU_MIX_QUAD) if quads else (VALU_MIX_HASH if hashed else VALU_MIX)
+    mix = VALU_MIX_HASH if hashed else VALU_MIX
     # frac: against the VALU-issue ceiling at the guide's max clock (2.4 GHz,
     # MI355X_MICROARCH.md) -- the peak the chip is specified for.  The clock
     # these launches actually held (in-kernel probe, gol_profile_clock) only
@@ -441,8 +443,7 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
          "valu": {"instructions_per_word_generation": {k: n for k, (n, _) in mix.items()},
                   "cycles_per_word_generation": round(cycles, 2),
                   "measured_valu_per_word_generation": round(pmc["valu_per_word_gen"], 2) if pmc else None,
-                  "circuit": ("per-row full-sum B3/S23 (rule_b3s23_fullsum), quad layout" if quads else
-                              "row-pair-shared B3/S23 (pair_sum + rule_b3s23_pair)"),
+                  "circuit": "row-pair-shared B3/S23 (pair_sum + rule_b3s23_pair)",
                   "source": "loop census scripts/isa_loop.py; issue costs profiles/r01_valu_op_costs.txt"},
          **common}
     held = {"clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None}
@@ -467,27 +468,20 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
     return r
 
 
-def quad_hg(ilv, plan):
-    """Do the plan's passes run the quad-layout horizontal-first kernel (half
-    the shifts: VALU_MIX_QUAD)?  Quads up to 8 generations per pass do."""
-    return ilv == 4 and bool(plan) and max(plan) <= 8
-
-
 def kernel_label(info, depths, ilv=2):
     """Name of the kernel instances the timed passes launch (depths: the pass
     plan, gol_pass_plan): the strip width (gol_occupancy) gives the words per
-    lane; multi-generation passes at 8-byte lanes or narrower, and on the quad
-    layout up to 8 generations, run the horizontal-first kernel (gol_capi.cpp
-    kernel_variant); ilv = the board's interleave (gol_device_layout)."""
+    lane; multi-generation passes at 8-byte lanes or narrower run the
+    horizontal-first kernel (gol_stencil.h launch_one); ilv = the board's
+    interleave (gol_device_layout)."""
     gs = sorted(set(depths)) or [1]
     waves, strip = info.get(gs[-1], (0, 0))
-    lay = {1: "row-major", 2: "pairs", 4: "quads"}.get(ilv, ilv)
+    lay = {1: "row-major", 2: "pairs"}.get(ilv, ilv)
     if gs == [1]:
         vec = strip // 64 if strip else "VEC"
         return f"gol::dev::step_kernel<{vec},LIFE,{lay}>"
     vec = strip // 62 if strip else 0
-    hg = os.environ.get("GOL_STENCIL_VARIANT", "2") != "1" and (vec in (1, 2) or (ilv == 4 and gs[-1] <= 8))
-    name = "multistep_hg_kernel" if hg else "multistep_kernel"
+    name = "multistep_hg_kernel" if vec in (1, 2) else "multistep_kernel"
     return f"gol::dev::{name}<{vec or 'VEC'},{'|'.join(map(str, gs))},LIFE,{lay}> ({waves} waves/CU resident)"
 
 
@@ -550,8 +544,7 @@ def secondary_run(GolEngine, a, local, parity=None):
         dt1, kms1, l1, g1, c1, _ = fresh_window(e2, None, n1, 0, a.hash, 50.0, 16)
         p1 = chk("65536^2 single-generation passes: gol_hash after K", shape, n1, e2.hash())
     sh = f"{S}x{S}"
-    ilv = N_layout(S)
-    r2 = roofline(kms2, l2, g2, S * S, plan2, sh, "N1", a.hash, c2, quad_hg(ilv, plan2))
+    r2 = roofline(kms2, l2, g2, S * S, plan2, sh, "N1", a.hash, c2)
     r1 = roofline(kms1, l1, g1, S * S, [1] * n1, sh, "N1", a.hash, c1)
     out.update({
         "value": round(S * S * n2 / dt2 / 1e9, 2), "unit": "GCUPS", "steps": n2,
@@ -629,7 +622,7 @@ def ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity):
         "unit": "GCUPS", "warmup": f"{a.warmup} ({warm}, after 1 s idle)", "ms_per_step": round(dt8 / a.steps * 1e3, 4),
         "pass_plan": plan8, "exchange": ring_stats(st8, l8), "parity": p8,
         "interior_launch": roofline(kms8, l8, g8, W * max(rows8 - round(2 * g8 / max(l8, 1)), 0), plan8,
-                                    f"{W}x{rows8}", "ring", False, c8, quad_hg(N_layout(W), plan8))}
+                                    f"{W}x{rows8}", "ring", False, c8)}
     return out
 
 
@@ -727,16 +720,15 @@ def main():
         hashed = {"value": round(vh, 2), "unit": "GCUPS", "ms_per_step": round(dth / a.steps * 1e3, 4),
                   "frac_of_unhashed": round(vh / value, 4), "pass_plan": hplan,
                   "roofline": roofline(kmsh, lh, gh, W * rows if world == 1 else W * max(rows - round(2 * gh / max(lh, 1)), 0),
-                                       hplan, f"{W}x{rows}", "N1" if world == 1 else "ring", True, ch,
-                                       quad_hg(ilv, hplan))}
+                                       hplan, f"{W}x{rows}", "N1" if world == 1 else "ring", True, ch)}
     # dominant kernel: the whole-shard (N=1) or interior-rows (N>1) launch of a
     # pass; G = generations that launch advances (the library's choice when --gpp 0)
     G = gcov / launches if launches else (a.gpp or 1)  # mean depth of the timed passes
     if world == 1:
-        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash, clk, quad_hg(ilv, plan))
+        roof = roofline(kms, launches, gcov, W * rows, plan, f"{W}x{rows}", "N1", a.hash, clk)
     else:
         roof = roofline(kms, launches, gcov, W * max(rows - round(2 * G), 0), plan, f"{W}x{rows}", "ring", a.hash,
-                        clk, quad_hg(ilv, plan))
+                        clk)
     if roof is not None:
         roof["kernel"] = kernel_label(eng_info, plan, ilv)
     ring = None
@@ -768,7 +760,7 @@ def main():
                                    f"row-block x{world}, G-deep RCCL halo send/recv per pass (ring over xGMI)"),
                    "generations_per_pass": round(G, 3), "band_rows": a.band or "auto",
                    "fused_hash": bool(a.hash),
-                   "layout": {1: "row-major", 2: "pairs", 4: "quads"}.get(ilv, ilv),
+                   "layout": {1: "row-major", 2: "pairs"}.get(ilv, ilv),
                    "window": "seed, 100 ms untimed settle, re-seed, W warm-up + K timed generations"},
         "roofline": roof,
         "parity": parity.report(),
@@ -807,9 +799,18 @@ def main():
         out["secondary"] = secondary
     if rank == 0 and world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(W, a.cpu_seconds)
+    # The compact parity verdict closes the line, so a tail of it always shows
+    # the headline's own check; a failed (or, without --allow-unchecked,
+    # unchecked) window fails the run after the line is printed.
+    failed = parity.failed(a.allow_unchecked)
+    out["parity_failed"] = failed
+    out["parity_ok"] = not failed
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(out) + "\n").encode())
+    if failed:
+        print(f"bench.py rank {rank}: parity failed: {failed}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -22,12 +22,21 @@
  * Host buffers (gol_load, gol_snapshot, checkpoints): bit-packed rows,
  * row = y, bit (x % 32) of 32-bit word (x / 32) is cell x (LSB first); words
  * per row = ceil(width / 32); bits at x >= width are zero.
- * Device layout (internal): the same rows, except that tori are kept
- * interleaved (gol_device_layout): quads when a row holds a multiple of 4
- * words -- word 4k + j holds columns 128k + 4b + j (bit b) -- else pairs when
- * it holds an even number -- word 2k + j holds columns 64k + 2b + j.  The
- * state hash is defined over these device words (DESIGN.md "State hash").
- * Two device planes (current / next) are swapped after every pass.
+ * Device layout (internal, a function of the geometry alone): the same rows,
+ * except that tori whose rows hold an even number of words are kept
+ * pair-interleaved (gol_device_layout) -- word 2k + j holds columns
+ * 64k + 2b + j (bit b).  Two device planes (current / next) are swapped after
+ * every pass.
+ *
+ * State hash (gol_hash, gol_step's per-generation hashes; DESIGN.md section
+ * 5): a function of the cells alone -- the same board at the same epoch
+ * hashes alike whatever the topology, layout, shard decomposition, pass
+ * depth or environment.  Columns 64g .. 64g + 63 of row y form group g, with
+ * canonical words E (bit b = cell 64g + 2b) and O (bit b = cell 64g + 2b + 1),
+ * cells past the width dead; then
+ *   hash = sum over (y, g) of (E A(y, 0) + O A(y, 1)) B(g)   (mod 2^64),
+ *   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * 0x9E3779B1 (mod 2^32),
+ *   A(y, 1) = A(y, 0) + 0x6A09E666,  B(g) = murmur3 fmix32(g + 0x7F4A7C15) | 1.
  */
 #ifndef GOL_H
 #define GOL_H
@@ -116,12 +125,12 @@ int gol_device_count(int* count);
  * host arithmetic.  Replaces the random placement of BoardCreator.scala:33-36. */
 int gol_shard_rows(int64_t height, int rank, int nranks, int64_t* row0, int64_t* rows);
 
-/* Device layout of a board (pure host arithmetic):
- * *words_per_group = 4 when a torus row holds whole quads of 32-bit words
- * (column 128g + 4b + j in bit b of word 4g + j), 2 when it holds whole
- * pairs (column 64g + 2b + j in bit b of word 2g + j), 1 (row-major: column
- * x in bit x % 32 of word x / 32) otherwise and on clipped boards.  The state
- * hash is defined over these device words (gol_hash, gol_step's hashes). */
+/* Device layout of a board (pure host arithmetic,
+ * informational): *words_per_group = 2 when a torus row holds whole pairs of
+ * 32-bit words (column 64g + 2b + j in bit b of word 2g + j), 1 (row-major:
+ * column x in bit x % 32 of word x / 32) otherwise and on clipped boards.
+ * Nothing at the boundary depends on it: host buffers are row-major and the
+ * state hash is defined over the cells. */
 int gol_device_layout(int32_t topology, int64_t width, int32_t* words_per_group);
 
 /* Seed the shard with the counter-based splitmix64 board (Bernoulli(0.5)),
@@ -356,10 +365,10 @@ int gol_runtime_info_get(gol_runtime_info* out);
  *                   automatic: the pass planner, see gol_pass_plan);
  *   words_per_lane  32-bit words each lane owns per row (1, 2 or 4; must
  *                   divide the words of a row).
- * GOL_EINVAL for words_per_lane = 4 together with gens_per_pass > 8 on any
+ * GOL_EINVAL for words_per_lane = 4 together with gens_per_pass > 7 on any
  * board but the B3/S23 torus: those kernel instances (generic rule masks,
- * clipped visibility) would spill registers to scratch (the planner never
- * picks them). */
+ * clipped visibility) would spill registers to scratch and are not built
+ * (the planner caps planned passes of such a tuning at 7). */
 int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32_t words_per_lane);
 
 /* Diagnostic: the pass depths (generations fused per HBM pass) gol_step would

@@ -280,24 +280,9 @@ void oracle_step_packed(const uint32_t* cur, uint32_t* nxt, int64_t W, int64_t H
 /* State hash (sharding-invariant, order-independent).                  */
 /* ------------------------------------------------------------------ */
 
-/* Device word order (DESIGN.md "Data layout"; gol_capi.cpp device_ilv): a
- * torus is stored interleaved in groups of k words -- columns 32k g .. 32k g +
- * 32k - 1 of a row live in words k g .. k g + k - 1, column 32k g + k b + j in
- * bit b of word k g + j -- with k = 2 (pairs) when its rows hold an even
- * number of words, or, with GOL_LAYOUT=quads in the environment (libgol's
- * opt-in quad layout), k = 4 when they hold a multiple of 4; every other
- * board is stored row-major (k = 1: bit x % 32 of word x / 32).  The hash is
- * defined over the device words, so the engine hashes without converting.
- * Returns k. */
-int oracle_device_ilv(int topology, int64_t wwords) {
-    const char* e = getenv("GOL_LAYOUT");
-    const int quads = e && strcmp(e, "quads") == 0;
-    if (topology != ORACLE_TORUS) return 1;
-    if (wwords % 4 == 0 && quads) return 4;
-    return wwords % 2 == 0 ? 2 : 1;
-}
-
-int oracle_pair_layout(int topology, int64_t wwords) { return oracle_device_ilv(topology, wwords) == 2; }
+/* The hash is a function of the logical board alone:
+ * it reads the cells through the canonical group words below, whatever
+ * layout, topology, shard decomposition or environment produced them. */
 
 static uint32_t even_bits(uint32_t x) { /* bits 0, 2, .., 30 -> bits 0 .. 15 */
     x &= 0x55555555u;
@@ -314,36 +299,21 @@ void oracle_to_pairs(uint32_t w0, uint32_t w1, uint32_t* e, uint32_t* o) {
     *o = even_bits(w0 >> 1) | (even_bits(w1 >> 1) << 16);
 }
 
-/* Device word j (0..3) of the quad whose row-major words w[0..3] hold
- * columns 0..127: bit b = column 4b + j, i.e. bit 4s + j of w[b / 8]
- * (s = b % 8).  Written bit by bit, independently of the device's shifts. */
-uint32_t oracle_quad_word(const uint32_t* w, int j) {
-    uint32_t q = 0;
-    for (int b = 0; b < 32; ++b) {
-        const int col = 4 * b + j;
-        q |= ((w[col / 32] >> (col % 32)) & 1u) << b;
-    }
-    return q;
+/* Canonical words of column group g of a row-major row of `wwords` words:
+ * the group is columns 64g .. 64g + 63, E holds its even columns (bit b =
+ * column 64g + 2b), O its odd ones (bit b = column 64g + 2b + 1).  A row
+ * with an odd number of words ends in a half group (its upper 16 bits 0). */
+void oracle_canonical_words(const uint32_t* row, int64_t wwords, int64_t g, uint32_t* e, uint32_t* o) {
+    const uint32_t w1 = 2 * g + 1 < wwords ? row[2 * g + 1] : 0u;
+    oracle_to_pairs(row[2 * g], w1, e, o);
 }
 
-/* Device word c of a row-major row (interleave k: 1, 2 or 4). */
-static uint32_t device_word(const uint32_t* row, int64_t c, int k) {
-    if (k == 1) return row[c];
-    const int64_t c0 = c - c % k;
-    if (k == 2) {
-        uint32_t e, o;
-        oracle_to_pairs(row[c0], row[c0 + 1], &e, &o);
-        return (c & 1) ? o : e;
-    }
-    return oracle_quad_word(row + c0, (int)(c % 4));
-}
-
-/* Keys of the state hash (DESIGN.md "State hash"; gol_kernels.h).  Device
- * word w at global row y and device word column c contributes
- *   w * A(y, c % G) * B(c / G)   (mod 2^64), G = 4 on the quad layout, else 2,
+/* Keys of the state hash (DESIGN.md "State hash"; gol_kernels.h).  The
+ * canonical words E, O of column group g of global row y contribute
+ *   (E * A(y, 0) + O * A(y, 1)) * B(g)     (mod 2^64),
  *   A(y, 0) = ((t ^ (t >> 15)) << 1) | 1,  t = y * 0x9E3779B1   (mod 2^32)
- *   A(y, j) = A(y, 0) + j * 0x6A09E666     (mod 2^32)
- *   B(k)    = fmix32(k + 0x7F4A7C15) | 1  (murmur3's 32-bit finaliser).
+ *   A(y, 1) = A(y, 0) + 0x6A09E666         (mod 2^32)
+ *   B(g)    = fmix32(g + 0x7F4A7C15) | 1  (murmur3's 32-bit finaliser).
  * Both keys are odd, so (A * B) is odd and any single-word difference changes
  * the sum; a sum commutes, so the value is the same for one shard or many and
  * for any evaluation order. */
@@ -363,23 +333,20 @@ uint32_t oracle_hash_pair_key(uint32_t k) {
     return h | 1u;
 }
 
-/* Rows [row0, row0+rows) of a row-major board with `wwords` words per row,
- * hashed over its device words of interleave `ilv` (1: row-major, 2: pairs,
- * 4: quads; oracle_device_ilv). */
+/* Rows [row0, row0+rows) of a row-major board with `wwords` words per row. */
 uint64_t oracle_hash_packed(const uint32_t* board, int64_t wwords, int64_t row0, int64_t rows,
-                            int64_t pitch, int ilv) {
-    const int k = ilv == 4 ? 4 : (ilv == 2 ? 2 : 1);
-    const int g = k == 4 ? 4 : 2; /* words per hash group */
+                            int64_t pitch) {
+    const int64_t groups = (wwords + 1) / 2;
     uint64_t h = 0;
     /* a sum mod 2^64 commutes: rows in parallel give the same value */
 #pragma omp parallel for schedule(static) reduction(+ : h) if (rows * wwords > (1 << 20))
     for (int64_t r = 0; r < rows; ++r) {
-        const uint32_t a0 = oracle_hash_row_key(row0 + r, 0);
-        for (int64_t c = 0; c < wwords; ++c) {
-            const uint32_t word = device_word(board + r * pitch, c, k);
-            const uint32_t a = a0 + (uint32_t)(c % g) * 0x6A09E666u;
-            const uint64_t key = (uint64_t)a * (uint64_t)oracle_hash_pair_key((uint32_t)(c / g));
-            h += (uint64_t)word * key;
+        const uint32_t a0 = oracle_hash_row_key(row0 + r, 0), a1 = oracle_hash_row_key(row0 + r, 1);
+        for (int64_t g = 0; g < groups; ++g) {
+            uint32_t e, o;
+            oracle_canonical_words(board + r * pitch, wwords, g, &e, &o);
+            const uint64_t b = oracle_hash_pair_key((uint32_t)g);
+            h += ((uint64_t)e * a0 + (uint64_t)o * a1) * b;
         }
     }
     return h;
@@ -392,12 +359,11 @@ void oracle_run_packed(uint32_t* board, uint32_t* tmp, int64_t W, int64_t H, int
                        int topology, uint32_t birth, uint32_t survive, int64_t vis_w,
                        int64_t vis_h, int64_t gens, uint64_t* hashes, int nthreads) {
     const int64_t wwords = (W + 31) / 32;
-    const int ilv = oracle_device_ilv(topology, wwords);
     uint32_t* a = board;
     uint32_t* b = tmp;
     for (int64_t g = 0; g < gens; ++g) {
         oracle_step_packed(a, b, W, H, pitch, topology, birth, survive, vis_w, vis_h, nthreads);
-        if (hashes) hashes[g] = oracle_hash_packed(b, wwords, 0, H, pitch, ilv);
+        if (hashes) hashes[g] = oracle_hash_packed(b, wwords, 0, H, pitch);
         uint32_t* t = a; a = b; b = t;
     }
     if (a != board) memcpy(board, a, (size_t)(H * pitch) * sizeof(uint32_t));

@@ -68,11 +68,8 @@ def lib():
         L.oracle_step_packed.argtypes = [_u32p, _u32p, _i64, _i64, _i64, ctypes.c_int,
                                          ctypes.c_uint32, ctypes.c_uint32, _i64, _i64, ctypes.c_int]
         L.oracle_hash_packed.restype = ctypes.c_uint64
-        L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64, ctypes.c_int]
-        L.oracle_pair_layout.argtypes = [ctypes.c_int, _i64]
-        L.oracle_device_ilv.argtypes = [ctypes.c_int, _i64]
-        L.oracle_quad_word.restype = ctypes.c_uint32
-        L.oracle_quad_word.argtypes = [_u32p, ctypes.c_int]
+        L.oracle_hash_packed.argtypes = [_u32p, _i64, _i64, _i64, _i64]
+        L.oracle_canonical_words.argtypes = [_u32p, _i64, _i64, _u32p, _u32p]
         L.oracle_hash_row_key.restype = ctypes.c_uint32
         L.oracle_hash_row_key.argtypes = [_i64, ctypes.c_int]
         L.oracle_hash_pair_key.restype = ctypes.c_uint32
@@ -168,68 +165,43 @@ def run_packed(packed: np.ndarray, W: int, gens: int, topology: int = TORUS, rul
     return board, hashes
 
 
-def device_ilv(W: int, topology: int = TORUS) -> int:
-    """Words per interleave group of the engine's device layout (gol_oracle.c
-    oracle_device_ilv): 2 (pairs) for a torus whose rows hold an even number
-    of words -- 4 (quads) for one holding a multiple of 4 with GOL_LAYOUT=quads
-    -- 1 (row-major) else."""
-    return int(lib().oracle_device_ilv(topology, wwords(W)))
-
-
-def pair_layout(W: int, topology: int = TORUS) -> bool:
-    """True when the engine stores the board pair-interleaved."""
-    return device_ilv(W, topology) == 2
-
-
 def hash_packed(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
-    """State hash of row-major packed rows [row0, row0 + rows) of a board
-    (over its device words: interleaved for tori, oracle_device_ilv)."""
+    """State hash of row-major packed rows [row0, row0 + rows) of a board: a
+    function of the cells alone, so `topology` does not
+    enter it (kept for the callers that pass it)."""
+    del topology
     packed = np.ascontiguousarray(packed, dtype=np.uint32)
     rows, pitch = packed.shape
-    return int(lib().oracle_hash_packed(_p(packed, _u32p), wwords(W), row0, rows, pitch,
-                                        device_ilv(W, topology)))
+    return int(lib().oracle_hash_packed(_p(packed, _u32p), wwords(W), row0, rows, pitch))
 
 
 # ------------------------------------------------- independent numpy restatement
 
-def np_ilv(W: int, topology: int = TORUS) -> int:
-    """numpy-side restatement of the layout rule: tori interleave groups of 2
-    words when a row holds whole pairs (4 when it holds whole quads and
-    GOL_LAYOUT=quads)."""
-    ww = wwords(W)
-    if topology != TORUS:
-        return 1
-    if ww % 4 == 0 and os.environ.get("GOL_LAYOUT") == "quads":
-        return 4
-    return 2 if ww % 2 == 0 else 1
-
-
-def np_device_words(packed: np.ndarray, W: int, topology: int = TORUS) -> np.ndarray:
-    """Row-major packed rows -> the engine's device words (independent numpy
-    restatement of the layout: with k words per group, column 32 k g + k b + j
-    -> bit b of word k g + j)."""
+def np_canonical_words(packed: np.ndarray, W: int) -> np.ndarray:
+    """Row-major packed rows -> the hash's canonical words (independent numpy
+    restatement): column 64 g + 2 b + j -> bit b of word 2 g + j, the row
+    padded with dead columns to whole 64-column groups."""
     ww = wwords(W)
     p = np.asarray(packed, dtype=np.uint32)[:, :ww]
-    k = np_ilv(W, topology)
-    if k == 1:
-        return p.copy()
-    rows = p.shape[0]
-    bits = ((p[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(rows, ww // k, 32 * k)
+    if ww % 2:
+        p = np.concatenate([p, np.zeros((p.shape[0], 1), dtype=np.uint32)], axis=1)
+    rows, nw = p.shape
+    bits = ((p[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(rows, nw // 2, 64)
     weights = np.uint64(1) << np.arange(32, dtype=np.uint64)
-    out = np.empty((rows, ww), dtype=np.uint32)
-    for j in range(k):
-        out[:, j::k] = (bits[:, :, j::k].astype(np.uint64) * weights).sum(axis=2).astype(np.uint32)
+    out = np.empty((rows, nw), dtype=np.uint32)
+    for j in range(2):
+        out[:, j::2] = (bits[:, :, j::2].astype(np.uint64) * weights).sum(axis=2).astype(np.uint32)
     return out
 
 
 def np_hash(packed: np.ndarray, W: int, row0: int = 0, topology: int = TORUS) -> int:
     """Same hash spec as gol_oracle.c (DESIGN.md "State hash"), written
-    independently with numpy: sum of w * A(y, c % G) * B(c / G) mod 2^64,
-    G = 4 on the quad layout, else 2."""
-    ww = wwords(W)
-    grp = 4 if np_ilv(W, topology) == 4 else 2
-    p = np_device_words(packed, W, topology).astype(np.uint64)
-    rows = p.shape[0]
+    independently with numpy: sum of w * A(y, c % 2) * B(c / 2) mod 2^64 over
+    the canonical words w (np_canonical_words)."""
+    del topology
+    grp = 2
+    p = np_canonical_words(packed, W).astype(np.uint64)
+    rows, ww = p.shape
     m32 = np.uint64(0xFFFFFFFF)
     with np.errstate(over="ignore"):
         y = np.arange(rows, dtype=np.uint64) + np.uint64(row0)

@@ -190,8 +190,10 @@ if __name__ == "__main__":
     sys.path.insert(0, ROOT)
     import bench
     sys.argv = ["bench.py"] + sys.argv[1:]
-    bench.main()
-    if "torch.distributed" in sys.modules:  # the stand-in all-reduce's group: tear it down before exit
-        import torch.distributed as dist
-        if dist.is_initialized():
-            dist.destroy_process_group()
+    try:
+        bench.main()
+    finally:
+        if "torch.distributed" in sys.modules:  # the stand-in all-reduce's group: tear it down before exit
+            import torch.distributed as dist
+            if dist.is_initialized():
+                dist.destroy_process_group()

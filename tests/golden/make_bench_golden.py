@@ -89,7 +89,7 @@ def main() -> None:
         L.oracle_step_packed(cur.ctypes.data_as(u32p), nxt.ctypes.data_as(u32p), W, H, ww, O.TORUS,
                              O.LIFE[0], O.LIFE[1], W, H, a.threads)
         cur, nxt = nxt, cur
-        hashes.append(int(L.oracle_hash_packed(cur.ctypes.data_as(u32p), ww, 0, H, ww, O.device_ilv(W))))
+        hashes.append(int(L.oracle_hash_packed(cur.ctypes.data_as(u32p), ww, 0, H, ww)))
         if g % 5 == 0 or g == a.gens:
             print(f"epoch {g}: {hashes[-1]:#018x}  ({time.time() - t0:.0f} s)", flush=True)
     block_check(cur, W, probe)

@@ -23,7 +23,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, tmp_path, *args, extra_env=None):
+def _run(world, tmp_path, *args, extra_env=None, rc=0):
     port = _free_port()
     procs = []
     for r in range(world):
@@ -33,7 +33,7 @@ def _run(world, tmp_path, *args, extra_env=None):
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=120) for p in procs]
     for p, (o, e) in zip(procs, outs):
-        assert p.returncode == 0, e[-2000:]
+        assert p.returncode == rc, e[-2000:]
     logs = [open(tmp_path / f"rank{r}.log").read().splitlines() for r in range(world)]
     return [o for o, _ in outs], logs
 
@@ -104,6 +104,8 @@ def test_multirank_bench_line(tmp_path, world):
     assert whats == [("65536x65536", 114, None), ("65536x65536", 1024, None), ("65536x65536", 256, None),
                      ("262144x262144", 25, None), ("262144x262144", None, [26, 50]), ("262144x262144", 50, None)]
     assert par["checks"][4]["checked"] == 25
+    # the compact verdict closes the line (the driver's tail shows it)
+    assert list(d)[-2:] == ["parity_failed", "parity_ok"] and d["parity_ok"] is True and d["parity_failed"] == []
     assert d["secondary"]["parity"]["match"] is True
     assert d["secondary"]["short_window"]["parity"]["epoch"] == 114
     assert d["secondary"]["single_generation_passes"]["parity"]["match"] is True
@@ -111,14 +113,18 @@ def test_multirank_bench_line(tmp_path, world):
 
 def test_multirank_bench_flags_a_wrong_shard(tmp_path):
     """A rank whose shard drifts from epoch 20 on (what a broken halo exchange
-    would do) turns parity.match false, and the mismatching epochs are named."""
-    outs, _ = _run(2, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
-                   extra_env={"FAKE_CORRUPT_RANK": "1"})
+    would do) turns parity.match false, the mismatching epochs are named, the
+    line closes with parity_ok false, and every rank exits non-zero after the
+    line is printed."""
+    outs, _ = _run(2, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary", "--no-fault",
+                   extra_env={"FAKE_CORRUPT_RANK": "1"}, rc=3)
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     par = d["parity"]
     assert par["match"] is False
     assert par["checks"][0]["match"] is False  # epoch 25
     assert par["checks"][1]["mismatched_epochs"][:2] == [26, 27]
+    assert list(d)[-1] == "parity_ok" and d["parity_ok"] is False
+    assert len(d["parity_failed"]) == 3 and all("mismatch" in f for f in d["parity_failed"])
 
 
 def test_single_rank_keeps_cpu_baseline_slot(tmp_path):

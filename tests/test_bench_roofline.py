@@ -54,13 +54,11 @@ def test_hashed_mix_adds_the_multiply_add():
     assert abs(c1 - c0 - 4.6) < 1e-9 and p1 < p0
 
 
-def test_pair_row_mix_and_quad_mix():
+def test_pair_row_mix():
     """The pair-layout mix is the row-pair-shared circuit's (8 full-rate logic
-    ops per word-generation, 26.8 cycles); the quad layout keeps the per-row
-    circuit (9 bitop3) with half the shifts."""
+    ops per word-generation, 26.8 cycles)."""
     _, c = bench.valu_peak_gcups(bench.VALU_MIX, 2.4)
-    _, cq = bench.valu_peak_gcups(bench.VALU_MIX_QUAD, 2.4)
-    assert abs(c - 26.8) < 1e-9 and abs(cq - 24.9) < 1e-9
+    assert abs(c - 26.8) < 1e-9
     assert sum(n for k, (n, _) in bench.VALU_MIX.items() if k not in ("v_alignbit_b32", "v_mov_b32_dpp")) == 8
 
 

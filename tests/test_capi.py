@@ -106,19 +106,20 @@ def test_codec_matches_oracle_layout():
         assert (codec.unpack(p, W) == c).all()
 
 
-def test_pair_layout_rule_matches_oracle():
-    # the host mirror of gol_create's layout rule and the oracle's hash layout agree
+def test_layout_rule_is_geometry_only(monkeypatch):
+    # libgol's own rule (gol_device_layout) and its Python restatement agree,
+    # and no environment variable moves it (round 4's GOL_LAYOUT is gone)
     from gameoflife import _native as N
-    from oracle import oracle as O
-    for w in (32, 64, 96, 128, 320, 352, 992, 1024, 4096, 65536, 262144):
-        assert N.pair_layout(w) == O.pair_layout(w, O.TORUS)
-        assert not N.pair_layout(w, N.GOL_REF_CLIPPED) and not O.pair_layout(w, O.REF_CLIPPED)
-        # libgol's own rule (gol_device_layout), its Python restatement, the oracle's
-        for topo in (N.GOL_TORUS, N.GOL_REF_CLIPPED):
-            k = N.device_layout(w, topo)
-            assert k == N.device_ilv(w, topo) == O.device_ilv(w, topo) == O.np_ilv(w, topo)
-    assert [N.device_layout(w) for w in (32, 64, 96, 128, 192, 256)] == [1, 2, 1, 2, 2, 2]
-    assert N.device_layout(128, N.GOL_REF_CLIPPED) == 1
+    for env in (None, "quads", "pairs"):
+        if env is None:
+            monkeypatch.delenv("GOL_LAYOUT", raising=False)
+        else:
+            monkeypatch.setenv("GOL_LAYOUT", env)
+        for w in (32, 64, 96, 128, 320, 352, 992, 1024, 4096, 65536, 262144):
+            for topo in (N.GOL_TORUS, N.GOL_REF_CLIPPED):
+                assert N.device_layout(w, topo) == N.device_ilv(w, topo)
+        assert [N.device_layout(w) for w in (32, 64, 96, 128, 192, 256)] == [1, 2, 1, 2, 2, 2]
+        assert N.device_layout(128, N.GOL_REF_CLIPPED) == 1
 
 
 def test_new_struct_layouts_match_header(tmp_path):

@@ -271,6 +271,27 @@ def test_fused_hash_equals_standalone_hash(gpu):
             assert h == e.hash()
 
 
+@pytest.mark.parametrize("W", [32 * 130, 32 * 129, 32 * 2, 32])
+def test_hash_is_a_function_of_the_cells(gpu, W):
+    """The state hash reads the cells through canonical words (DESIGN.md
+    section 5): the same cells held by a pair-layout torus (even word count),
+    a row-major torus (odd word count) and a row-major clipped board hash
+    alike -- gol_hash and the fused per-generation hashes of the identity
+    rule, which keeps the board -- and equal the oracle's value."""
+    from gameoflife import _native as N
+    rng = np.random.default_rng(W)
+    cells = (rng.random((23, W)) < 0.5).astype(np.uint8)
+    board = O.pack(cells)
+    want = O.hash_packed(board, W)
+    got = {}
+    for topo in ("torus", "ref-clipped"):
+        with engine(W, 23, topology=topo, rule=rule_obj(O.REF_EFFECTIVE)) as e:
+            e.load(board)
+            got[topo] = (e.hash(), [int(x) for x in e.step(3, hashes=True)])
+    assert got["torus"] == got["ref-clipped"] == (want, [want] * 3)
+    assert N.device_layout(W) == (2 if (W // 32) % 2 == 0 else 1) and N.device_layout(W, N.GOL_REF_CLIPPED) == 1
+
+
 def test_snapshot_get_cell_checkpoint(gpu):
     W, H = 32 * 70, 50
     with engine(W, H) as e:

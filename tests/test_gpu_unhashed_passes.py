@@ -20,10 +20,9 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-# words per row: one pair / one quad; under one wave; 62 / 63 / 64 pairs; exact
-# multiples of the 124-word pair strip and the 248-word quad strip (and of 126)
-# and either side of them; many strips (tests/test_gpu_quads.py runs the same
-# list on the opt-in quad layout).
+# words per row: one pair / two pairs; under one wave; 62 / 63 / 64 pairs; exact
+# multiples of the 124-word pair strip and of 248 (and of 126) and either side
+# of them; many strips.
 WORDS = [2, 4, 60, 122, 124, 126, 128, 244, 246, 248, 250, 252, 254, 372, 378, 380, 492, 496, 500, 1024, 8190, 8192]
 DEPTHS = list(range(2, 13))
 
@@ -56,8 +55,7 @@ def test_strip_geometry(gpu):
     """gol_occupancy reports 124-word strips (62 output lanes x 2 words) for
     multi-generation passes on the pair layout, 128 or 256 (64 lanes) for
     single-generation passes and 62 (one word per lane) where the layout is
-    row-major (odd word count); the opt-in quad layout's 248-word strips are
-    checked in tests/test_gpu_quads.py."""
+    row-major (odd word count)."""
     for words in (8192, 8190):
         with engine(32 * words, 16) as e:
             for g in DEPTHS:

@@ -1,5 +1,6 @@
 """CPU tests of the oracle: restatements agree, known-answer patterns hold,
 and the committed golden vectors reproduce.  (No GPU.)"""
+import ctypes
 import json
 import os
 
@@ -97,17 +98,25 @@ def test_blinker_block_glider_torus():
     assert (O.unpack(p, W) == glider).all()  # full wrap after 4N generations
 
 
-def test_pair_layout_rule():
-    # device words are pair-interleaved exactly for tori of even word width
-    assert O.pair_layout(64) and O.pair_layout(320) and not O.pair_layout(32) and not O.pair_layout(96)
-    assert not O.pair_layout(64, O.REF_CLIPPED)
-    # numpy restatement of the interleave: column 64k + 2b -> bit b of word 2k, 64k + 2b + 1 -> word 2k + 1
-    cells = np.random.default_rng(3).integers(0, 2, size=(5, 192), dtype=np.uint8)
-    dev = O.np_device_words(O.pack(cells), 192)
-    for y in range(5):
-        for x in range(192):
-            word, bit = 2 * (x // 64) + (x & 1), (x % 64) >> 1
-            assert (int(dev[y, word]) >> bit) & 1 == cells[y, x]
+def test_canonical_words():
+    # numpy restatement of the hash's canonical words: column 64k + 2b -> bit b
+    # of word 2k, 64k + 2b + 1 -> word 2k + 1; the C oracle's agree
+    rng = np.random.default_rng(3)
+    for W in (192, 160, 32, 33, 300):
+        cells = rng.integers(0, 2, size=(5, W), dtype=np.uint8)
+        packed = O.pack(cells)
+        dev = O.np_canonical_words(packed, W)
+        ww = (W + 31) // 32
+        assert dev.shape == (5, ww + (ww % 2))
+        for y in range(5):
+            for x in range(dev.shape[1] * 32):
+                word, bit = 2 * (x // 64) + (x & 1), (x % 64) >> 1
+                assert (int(dev[y, word]) >> bit) & 1 == (cells[y, x] if x < W else 0)
+            for g in range(dev.shape[1] // 2):
+                e, o = ctypes.c_uint32(), ctypes.c_uint32()
+                O.lib().oracle_canonical_words(packed[y].ctypes.data_as(O._u32p), ww, g, ctypes.byref(e),
+                                               ctypes.byref(o))
+                assert (e.value, o.value) == (int(dev[y, 2 * g]), int(dev[y, 2 * g + 1]))
 
 
 def test_hash_properties():
@@ -117,7 +126,9 @@ def test_hash_properties():
     b = O.seed_packed(320, 40, 1)
     h = O.hash_packed(b, 320)
     assert h == O.np_hash(b, 320)
-    assert h != O.hash_packed(b, 320, topology=O.REF_CLIPPED)  # pair-interleaved vs row-major words
+    # a function of the cells alone: the topology (hence the engine's device
+    # layout) does not enter it
+    assert h == O.hash_packed(b, 320, topology=O.REF_CLIPPED)
     # sharding invariance: partial hashes of row blocks sum to the whole
     parts = [O.hash_packed(b[r0:r1], 320, row0=r0) for r0, r1 in [(0, 7), (7, 30), (30, 40)]]
     assert sum(parts) % (1 << 64) == h
@@ -127,6 +138,14 @@ def test_hash_properties():
         y, x = int(rng.integers(0, 40)), int(rng.integers(0, 320))
         b2 = b.copy(); b2[y, x // 32] ^= np.uint32(1 << (x % 32))
         assert O.hash_packed(b2, 320) != h
+    # the pitch and dead padding words past the width do not enter it
+    wide = np.zeros((40, 16), dtype=np.uint32); wide[:, :10] = b
+    assert O.hash_packed(wide[:, :10], 320) == h
+    # a board W cells wide and the same cells in a wider board (dead columns
+    # beyond W) hash alike -- including an odd word count's half group
+    b3 = O.seed_packed(96, 8, 5)
+    b4 = np.zeros((8, 4), dtype=np.uint32); b4[:, :3] = b3
+    assert O.hash_packed(b3, 96) == O.hash_packed(b4, 128) == O.np_hash(b4, 128) == O.np_hash(b3, 96)
 
 
 def test_hash_keys_odd_and_structured_moves_detected():
