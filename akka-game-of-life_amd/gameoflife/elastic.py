@@ -83,6 +83,16 @@ def make_checkpoint(h: dict, packed: np.ndarray) -> bytes:
     return hdr + np.ascontiguousarray(packed, dtype=np.uint32).tobytes()
 
 
+def checkpoint_buffer(h: dict, rows: int, wwords: int) -> tuple[np.ndarray, np.ndarray]:
+    """An empty gol_checkpoint blob for header fields `h` (row0, epoch, ...)
+    and `rows` rows: (the blob as uint8, its rows as a (rows, wwords) uint32
+    view to fill in place -- snapshot(out=...) slices -- with no extra copy)."""
+    blob = np.empty(_HDR.size + rows * wwords * 4, dtype=np.uint8)
+    _HDR.pack_into(blob, 0, _MAGIC, h["width"], h["height"], h["row0"], rows, wwords, h["epoch"], h["topology"],
+                   h["birth"], h["survive"], 0)
+    return blob, blob[_HDR.size:].view(np.uint32).reshape(rows, wwords)
+
+
 def epoch_dir(ckpt_dir: str, epoch: int) -> str:
     return os.path.join(ckpt_dir, f"e{epoch:09d}")
 
@@ -644,6 +654,131 @@ class Supervisor:
                 e, h = line.split()
                 out[int(e)] = int(h)
         return out
+
+
+# ----------------------------------------------------------- one process per GPU
+
+def ring_fault_drill(eng, make_engine, join, rank: int, world: int, width: int, height: int, ckpt_dir: str, *,
+                     seed: int = 0x5EED, victim: int = 3, kill_at: int = 25, gens: int = 50, every: int = 10,
+                     topology: str = "torus"):
+    """BASELINE.json config 5 in the form the multi-GPU bench runs it: the
+    ranks of one job (one process per GPU, no supervisor) lose one of their
+    backends mid-run and re-spawn its shard on a surviving GPU.
+
+    Every rank seeds its shard and steps with fused hashes, all-reducing the
+    partials into the global per-generation hashes and writing its shard
+    checkpoint every `every` generations into `ckpt_dir` (a directory all
+    ranks share).  After generation `kill_at` rank `victim` (capped at
+    world - 1) drops its communicator and its context -- a backend lost
+    between two steps, before it could checkpoint (the process itself stays
+    alive, so the launcher does not tear the job down).  Then, as in
+    ``BoardCreator.onCellTermination`` (BoardCreator.scala:120-154):
+
+    * the survivors leave the old ring (gol_comm_abort);
+    * the rank whose rows adjoin the lost block (the one above it; for rank 0
+      the one below) restores the block's last checkpoint c <= kill_at, takes
+      the kill_at - c rows above and below it at epoch c from the
+      neighbours' checkpoint files (the light cone) and replays the block
+      alone to kill_at (gol_replay; CellActor.scala:34,71-74,86 is the
+      history replay it stands for), then holds its own rows and the lost
+      ones as one context on its GPU -- nobody else rolls back;
+    * the survivors join a new world - 1 rank ring (`join`, ranks renumbered
+      in row order) and step on to `gens`.
+
+    eng: this rank's context, already in the `world`-rank ring (rows of
+    gol_shard_rows).  make_engine(row0, rows): a new context on this GPU.
+    join(eng, tag, rank, world): put `eng` into the ring `tag`.
+
+    Returns (the rank's context afterwards -- None for the lost rank, whose
+    context is gone --, report).  The report holds the global hashes the
+    caller checks: `before` (epochs 1..kill_at), `replayed` (epochs
+    c + 1..kill_at: the replayed block's partials plus the survivors'),
+    `at_recovery` (gol_hash over the new ring at kill_at), `after` (epochs
+    kill_at + 1..gens) and `final` (gol_hash at gens), with wall times."""
+    torus = topology == "torus"
+    victim = max(0, min(victim, world - 1))
+    host = victim - 1 if victim > 0 else 1
+    row0, rows = shard_rows_py(height, rank, world)
+    rep = {"victim_rank": victim, "host_rank": host, "world_before": world, "world_after": world - 1,
+           "kill_at": kill_at, "generations": gens, "checkpoint_every": every}
+    eng.seed(seed)
+    epoch, before, parts = 0, [], {}
+    my_file, ckpt_s = None, 0.0
+    t_run = time.perf_counter()
+    while epoch < kill_at:
+        n = min(every - epoch % every, kill_at - epoch)
+        part = eng.step(n, hashes=True)
+        glob = eng.allreduce_u64(part)
+        for k in range(n):
+            parts[epoch + k + 1] = int(part[k])
+        before.extend(int(x) for x in glob)
+        epoch += n
+        # a checkpoint every `every` generations; the lost rank dies right
+        # after its last step, before it could write one
+        if epoch % every == 0 and not (rank == victim and epoch == kill_at):
+            t = time.perf_counter()
+            path = write_shard_checkpoint(ckpt_dir, eng.checkpoint())
+            if my_file and my_file != path:
+                os.unlink(my_file)  # every rank passed this epoch's checkpoint before the next step
+            my_file, ckpt_s = path, ckpt_s + time.perf_counter() - t
+    rep["before"] = before
+    rep["checkpoint_s"] = round(ckpt_s, 3)
+    rep["run_to_loss_s"] = round(time.perf_counter() - t_run, 3)
+    if rank == victim:
+        eng.comm_abort()
+        eng.close()
+        rep["role"] = "lost"
+        return None, rep
+    # -- recovery on the survivors
+    t_loss = time.perf_counter()
+    eng.comm_abort()
+    new_rank, new_world = (rank if rank < victim else rank - 1), world - 1
+    v0, vn = shard_rows_py(height, victim, world)
+    c, hs = 0, None
+    if rank == host:
+        c = recovery_epoch(ckpt_dir, v0, v0 + vn, epoch, height, torus)
+        d = epoch - c
+        blob = assemble_checkpoint(ckpt_dir, c, v0, vn)
+        above, below = light_cone(ckpt_dir, c, v0, vn, d, height, torus)
+        h, _ = parse_checkpoint(blob)
+        r = make_engine(v0, vn)
+        try:
+            r.restore(blob)
+            hs = r.replay(d, above, below) if d else np.zeros(0, dtype=np.uint64)
+            del blob
+            lost_first = v0 + vn == row0  # the lost block lies above this one (victim 0, host 1)
+            nrow0 = v0 if lost_first else row0
+            merged, data = checkpoint_buffer(dict(h, row0=nrow0, epoch=epoch), rows + vn, h["wwords"])
+            r.snapshot(out=data[:vn] if lost_first else data[rows:])
+        finally:
+            r.close()
+        eng.snapshot(out=data[vn:] if lost_first else data[:rows])
+        eng.close()
+        row0, rows = nrow0, rows + vn
+        eng = make_engine(row0, rows)
+        eng.restore(merged)
+        del merged, data
+        rep["replay_s"] = round(time.perf_counter() - t_loss, 3)
+    join(eng, "fault", new_rank, new_world)
+    t_ready = time.perf_counter()
+    # the checkpoint epoch the host replayed from, to every survivor
+    c = int(eng.allreduce_u64(np.array([c], dtype=np.uint64))[0])
+    mine = np.array([parts[e] for e in range(c + 1, epoch + 1)], dtype=np.uint64)
+    if hs is not None:
+        mine = mine + hs  # mod 2^64
+    rep["checkpoint_epoch"] = c
+    rep["replayed_generations"] = epoch - c
+    rep["replayed"] = [int(x) for x in eng.allreduce_u64(mine)]
+    rep["at_recovery"] = int(eng.allreduce_u64(np.array([eng.hash()], dtype=np.uint64))[0])
+    rep["recovery_s"] = t_ready - t_loss  # this rank's; the caller takes the max
+    rep["rows_after"] = [row0, rows]
+    t1 = time.perf_counter()
+    part = eng.step(gens - epoch, hashes=True) if gens > epoch else np.zeros(0, dtype=np.uint64)
+    rep["after"] = [int(x) for x in eng.allreduce_u64(part)] if gens > epoch else []
+    rep["after_s"] = time.perf_counter() - t1
+    rep["final"] = int(eng.allreduce_u64(np.array([eng.hash()], dtype=np.uint64))[0])
+    rep["role"] = "host" if rank == host else "survivor"
+    return eng, rep
 
 
 # ----------------------------------------------------------- CLI

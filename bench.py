@@ -91,24 +91,29 @@ def parse():
     ap.add_argument("--no-ring", action="store_true", help="skip the N = 1 ring-schedule measurements")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-fault", action="store_true",
+                    help="skip the N > 1 fault drill (config 5: a rank lost at generation 25 of 50, its shard "
+                         "re-spawned on a surviving GPU)")
     ap.add_argument("--allow-unchecked", action="store_true",
                     help="exit 0 when a window has no golden value (boards without a table); a mismatch still fails")
     return ap.parse_args()
 
 
 class Job:
-    """This process's place in the launch (one process per GPU).
+    """This process's place in the launch (one process per GPU, one node).
 
     Ranks come from the launcher's environment (torch.distributed.run sets
-    RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  Rank 0's RCCL
-    unique id reaches the other ranks through a file named after
-    MASTER_ADDR:MASTER_PORT (one node; under torch.distributed.run also
-    after the elastic agent, the ranks' common parent); a file older than this rank's start
-    (minus two minutes of launch skew) is a leftover of an earlier job and is
-    ignored.  After the first barrier over the new communicator every rank
-    has read it, and rank 0 removes it.  Barriers and the
-    max over ranks are gol_comm_allreduce_u64 calls on the shard's own RCCL
-    communicator: no torch, no second collective library."""
+    RANK, WORLD_SIZE, LOCAL_RANK, LOCAL_WORLD_SIZE, MASTER_ADDR, MASTER_PORT).
+    Rank 0's RCCL unique id reaches the other ranks through a file in the
+    node's temp directory named after MASTER_ADDR:MASTER_PORT and the launch:
+    the ranks' common parent (torch.distributed.run's elastic agent, or
+    whatever started them) or GOL_BENCH_RUN_ID when set, so a file a crashed
+    earlier job left behind on the same port is never read; a file older than
+    this rank's start (minus two minutes of launch skew) is ignored as well.
+    After the first barrier over the new communicator every rank has read it,
+    and rank 0 removes it.  Barriers and the max over ranks are
+    gol_comm_allreduce_u64 calls on the shard's own RCCL communicator: no
+    torch, no second collective library."""
 
     def __init__(self, n):
         self.rank = int(os.environ.get("RANK", "0"))
@@ -116,23 +121,29 @@ class Job:
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         if self.world != n:
             raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(self.world)))
+        if self.world > local_world:
+            raise SystemExit(f"WORLD_SIZE={self.world} > LOCAL_WORLD_SIZE={local_world}: bench.py's rendezvous "
+                             "(a file in this node's temp directory) serves one node only")
         self.eng = None  # the engine whose communicator carries the collectives
         self.t_start = time.time()
 
-    def uid_path(self):
-        # Under torch.distributed.run every local rank is a child of the same
-        # elastic agent, so the agent's pid tells this job's file from one a
-        # crashed earlier job on the same port left behind (its run id is
-        # "none" unless --rdzv-id is given).  Other launchers: address + port.
-        agent = str(os.getppid()) if "TORCHELASTIC_RUN_ID" in os.environ else ""
-        key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"),
-                        os.environ.get("TORCHELASTIC_RUN_ID", ""), agent])
+    def uid_path(self, tag=""):
+        # The launch key: under torch.distributed.run every local rank is a
+        # child of the same elastic agent (its run id is "none" unless
+        # --rdzv-id is given); other launchers' ranks share their launcher as
+        # parent too, unless GOL_BENCH_RUN_ID names the launch explicitly.
+        launch = os.environ.get("GOL_BENCH_RUN_ID") or f"{os.environ.get('TORCHELASTIC_RUN_ID', '')}_{os.getppid()}"
+        key = "_".join([os.environ.get("MASTER_ADDR", "127.0.0.1"), os.environ.get("MASTER_PORT", "0"), launch, tag])
         return os.path.join(tempfile.gettempdir(), "gol_bench_uid_" + hashlib.sha1(key.encode()).hexdigest()[:16])
 
-    def join(self, eng, N, timeout=300.0):
-        """Attach `eng` to the job's RCCL ring (rank 0 makes the id)."""
-        path = self.uid_path()
-        if self.rank == 0:
+    def join(self, eng, N, timeout=300.0, tag="", rank=None, world=None):
+        """Attach `eng` to the job's RCCL ring (rank 0 makes the id); `tag`,
+        `rank`, `world`: a later ring of the same job (the fault drill's)."""
+        path = self.uid_path(tag)
+        rank = self.rank if rank is None else rank
+        world = self.world if world is None else world
+        if rank == 0:
             uid = N.unique_id()
             tmp = f"{path}.{os.getpid()}.tmp"
             with open(tmp, "wb") as f:
@@ -150,16 +161,18 @@ class Job:
                 except OSError:
                     pass
                 if time.monotonic() - t0 > timeout:
-                    raise SystemExit(f"rank {self.rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s")
+                    raise SystemExit(f"rank {rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s")
                 time.sleep(0.01)
-        eng.comm_init(uid, self.rank, self.world)
-        self.eng = eng
-        self.barrier()  # every rank has read the id
-        if self.rank == 0:
+        eng.comm_init(uid, rank, world)
+        if world > 1:
+            eng.allreduce_u64([0])  # every rank has read the id
+        if rank == 0:
             try:
                 os.unlink(path)
             except OSError:
                 pass
+        if not tag:
+            self.eng = eng
 
     def barrier(self):
         if self.world > 1:
@@ -653,6 +666,77 @@ def rank_table(job, N, stats, dt, info):
     return job.gather(row)
 
 
+def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
+    """BASELINE.json configs[4] at N > 1, after the timed windows: the ranks
+    lose rank min(3, N - 1) after generation 25 of 50 (checkpoints every 10)
+    and re-spawn its shard on the rank above it, which replays it alone from
+    its checkpoint and the light cone; the N - 1 survivors rebuild the RCCL
+    ring and step on to 50 (gameoflife.elastic.ring_fault_drill; the
+    reference's re-deploy of a dead cell, BoardCreator.scala:120-154).  Every
+    global hash is checked against bench_262144.json.  Returns (the sub-line
+    or None off rank 0, this rank's context afterwards -- None on the lost
+    rank)."""
+    import shutil
+    import numpy as np
+    from gameoflife.elastic import ring_fault_drill
+    ckpt = job.uid_path("fault_ckpt") + "_dir"  # one node: the ranks share the temp directory
+    if job.rank == 0:
+        shutil.rmtree(ckpt, ignore_errors=True)
+        os.makedirs(ckpt)
+    job.barrier()
+    make = lambda r0, n: GolEngine(W, H, topology="torus", rule="life", device=local, row0=r0, rows=n)  # noqa: E731
+    join = lambda e, tag, r, w: job.join(e, N, tag=tag, rank=r, world=w)  # noqa: E731
+    t0 = time.perf_counter()
+    eng, rep = ring_fault_drill(eng, make, join, job.rank, job.world, W, H, ckpt, seed=GOLDEN_SEED, victim=3,
+                                kill_at=25, gens=50, every=10)
+    if eng is None:  # the lost rank: its context is gone, it sits out the rest
+        return None, None
+    nw, nr = rep["world_after"], job.rank if job.rank < rep["victim_rank"] else job.rank - 1
+
+    def ring_max(x):
+        row = np.zeros(nw, dtype=np.uint64)
+        row[nr] = round(x * 1e9)
+        return float(eng.allreduce_u64(row).max()) / 1e9 if nw > 1 else x
+
+    rec, aft, ck = ring_max(rep["recovery_s"]), ring_max(rep["after_s"]), ring_max(rep["checkpoint_s"])
+    wall = ring_max(time.perf_counter() - t0)
+    shape, c, k = (W, H), rep["checkpoint_epoch"], rep["kill_at"]
+    checks = [
+        parity.sequence("fault drill: global hashes before the loss (every rank)", shape, 1, rep["before"]),
+        parity.sequence("fault drill: the replayed block's partials + the survivors' (epochs after the checkpoint)",
+                        shape, c + 1, rep["replayed"]),
+        {**parity.board("fault drill: gol_hash over the rebuilt ring at the loss epoch", shape, k,
+                        rep["at_recovery"]), "what": "at recovery"},
+        parity.sequence("fault drill: fused hashes on the rebuilt ring", shape, k + 1, rep["after"]),
+        {**parity.board("fault drill: gol_hash at the end", shape, rep["generations"], rep["final"]), "what": "final"},
+    ]
+    if job.rank == 0:
+        shutil.rmtree(ckpt, ignore_errors=True)  # every survivor has read what it needed
+    if job.rank != 0:
+        return None, eng
+    after_gens = rep["generations"] - k
+    ms = [c_.get("match") for c_ in checks]
+    return {
+        "workload": f"{W}x{H} torus B3/S23 over {job.world} ranks: rank {rep['victim_rank']} lost after generation "
+                    f"{k} of {rep['generations']} (BASELINE.json configs[4]), its shard re-spawned on rank "
+                    f"{rep['host_rank']}'s GPU, {nw} ranks after",
+        "checkpoint_every": rep["checkpoint_every"], "checkpoint_epoch": c,
+        "replayed_generations": rep["replayed_generations"], "world_after": nw,
+        "checkpoint_s_max": round(ck, 3),
+        "recovery_ms": round(rec * 1e3, 1),
+        "after": {"generations": after_gens, "ms_per_step": round(aft / max(after_gens, 1) * 1e3, 4),
+                  "value": round(W * H * after_gens / aft / 1e9, 2) if aft > 0 else None, "unit": "GCUPS",
+                  "note": "fused per-generation hashes on the N - 1 ring, one rank holding two shards"},
+        "wall_s": round(wall, 3),
+        "parity": {"match": None if any(m is None for m in ms) else all(ms),
+                   "checks": [{kk: c_[kk] for kk in ("epochs", "epoch", "checked", "mismatched_epochs", "match")
+                               if kk in c_} for c_ in checks]},
+        "note": "recovery_ms: loss -> the host replayed the lost block (gol_replay from its checkpoint and the "
+                "light cone read back from the checkpoint files) and merged it, and the survivors joined the "
+                "new RCCL ring (max over the survivors)",
+    }, eng
+
+
 def main():
     a = parse()
     # one JSON line on stdout: native libraries (RCCL's version banner at
@@ -793,7 +877,12 @@ def main():
     if ring is not None:
         out["ring_schedule_n1"] = ring
     job.barrier()
-    eng.close()
+    if world > 1 and not a.no_fault:
+        fault, eng = fault_drill(job, N, GolEngine, eng, a, W, H, local, parity)
+        if fault is not None:
+            out["fault_recovery"] = fault
+    if eng is not None:
+        eng.close()
 
     if rank == 0 and secondary is not None:
         out["secondary"] = secondary

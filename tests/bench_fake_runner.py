@@ -39,36 +39,87 @@ def golden(width, height):
         return [int(x, 16) for x in json.load(f)["hashes"]]
 
 
+def _mix(x):
+    """splitmix64's finaliser on a uint64 array (wraps mod 2^64)."""
+    with np.errstate(over="ignore"):
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+class FakeBoard:
+    """A W x Hb torus whose "cells" are one u64 per row, c(y, e) at epoch e:
+    pseudo-random for y > 0, and row 0 carries the rest of the golden hash of
+    epoch e -- so the sum over any decomposition of the rows is the golden
+    value, and only the whole sum is (a partial sum is a meaningless share).
+    A row's data is its u64 as two u32 words (wwords = 2)."""
+
+    _rest = {}
+
+    def __init__(self, width, hb):
+        self.w, self.hb = width, hb
+        self.table = golden(width, hb)
+
+    def rows(self, ys, e):
+        ys = np.asarray(ys, dtype=np.int64) % self.hb
+        with np.errstate(over="ignore"):
+            v = _mix(ys.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(e + 1) * np.uint64(0xD1B54A32D192ED03)
+                     + np.uint64(self.hb))
+        if (ys == 0).any():
+            key = (self.w, self.hb, e)
+            if key not in self._rest:
+                with np.errstate(over="ignore"):
+                    rest = int(_mix(np.arange(1, self.hb, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+                                    + np.uint64(e + 1) * np.uint64(0xD1B54A32D192ED03) + np.uint64(self.hb)).sum())
+                self._rest[key] = rest & M64
+            g = self.table[e] if e < len(self.table) else 0
+            v[ys == 0] = np.uint64((g - self._rest[key]) & M64)
+        return v
+
+    def block_sum(self, row0, rows, e):
+        with np.errstate(over="ignore"):
+            return int(self.rows(np.arange(row0, row0 + rows), e).sum()) & M64
+
+    @staticmethod
+    def words(v):
+        return np.stack([(v & np.uint64(0xFFFFFFFF)).astype(np.uint32), (v >> np.uint64(32)).astype(np.uint32)], axis=1)
+
+
 class FakeEngine:
-    """Records calls; its state hash is a share of the golden hash of its
-    epoch: rank r > 0 holds a pseudo-random share, rank 0 the rest, so only
-    the sum over all ranks (the all-reduce) equals the golden value."""
+    """Records calls; its state is a block of FakeBoard rows at an epoch: the
+    state hash is the block's sum (so only the sum over all ranks -- the
+    all-reduce -- equals the golden value), checkpoints / snapshots carry the
+    rows' words, restore checks that a blob holds exactly the rows of its
+    block at its epoch, and replay checks the light cone it is handed -- so
+    the fault drill's bookkeeping (which rows, which epoch, merged in which
+    order) is checked, not just its control flow."""
+
+    wwords = 2
 
     def __init__(self, width, height, topology="torus", rule="life", device=0, row0=0, rows=0):
-        self.w, self.h, self.rows = width, height, rows or height
+        self.w, self.h, self.row0, self.rows = width, height, row0, rows or height
         self.gens = self.launches = 0
         self.ms = 0.0
         self.epoch = 0
         self.whole = self.rows == height
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        # in a multi-rank job a shard is rows of the global torus; alone, a
+        # context with fewer rows is a torus of its own height (as libgol's)
+        self.board = FakeBoard(width, height if world > 1 else self.rows)
+        if world == 1:
+            self.row0 = 0
+        self.corrupt = os.environ.get("FAKE_CORRUPT_RANK") == str(RANK)
         log("create", f"{width}x{self.rows}", "device", device, "row0", row0)
 
-    def _share(self, epoch):
-        world = int(os.environ.get("WORLD_SIZE", "1"))
-        if self.whole or world == 1:
-            g = golden(self.w, self.rows)
-            return g[epoch] if epoch < len(g) else 0
-        others = [(0x9E3779B97F4A7C15 * (epoch + 1) * (r + 7)) & M64 for r in range(1, world)]
-        if RANK > 0:
-            # FAKE_CORRUPT_RANK: this rank's shard goes wrong from epoch 20 on
-            # (a halo-exchange bug), which the summed hash must expose
-            bad = os.environ.get("FAKE_CORRUPT_RANK") == str(RANK) and epoch >= 20
-            return (others[RANK - 1] + (1 if bad else 0)) & M64
-        g = golden(self.w, self.h)
-        return ((g[epoch] if epoch < len(g) else 0) - sum(others)) & M64
+    def _hash(self, epoch):
+        # FAKE_CORRUPT_RANK: this rank's shard goes wrong from epoch 20 on
+        # (a halo-exchange bug), which the summed hash must expose
+        bad = 1 if self.corrupt and epoch >= 20 else 0
+        return (self.board.block_sum(self.row0, self.rows, epoch) + bad) & M64
 
     def hash(self):
         log("hash", f"{self.w}x{self.rows}", self.epoch)
-        return self._share(self.epoch)
+        return self._hash(self.epoch)
 
     def allreduce_u64(self, values):
         import torch
@@ -76,8 +127,8 @@ class FakeEngine:
         v = np.asarray(values, dtype=np.uint64)
         lo = torch.tensor((v & np.uint64(0xFFFFFFFF)).astype(np.int64))
         hi = torch.tensor((v >> np.uint64(32)).astype(np.int64))
-        dist.all_reduce(lo)
-        dist.all_reduce(hi)
+        dist.all_reduce(lo, group=_GROUP)
+        dist.all_reduce(hi, group=_GROUP)
         log("allreduce", len(v))
         out = [((int(h) << 32) + int(l)) & M64 for l, h in zip(lo.tolist(), hi.tolist())]
         return np.array(out, dtype=np.uint64)
@@ -96,6 +147,14 @@ class FakeEngine:
 
     def comm_init(self, uid, rank, world):
         log("comm_init", uid.hex()[:16], rank, world)
+        _join(rank, world)
+
+    def comm_abort(self):
+        log("comm_abort", f"{self.w}x{self.rows}")
+        full = int(os.environ.get("WORLD_SIZE", "1"))
+        if full > 1 and RANK == _lost_rank(full):
+            import torch.distributed as dist
+            dist.new_group([r for r in range(full) if r != RANK])  # collective: the survivors' next ring
 
     def seed(self, seed):
         self.epoch = 0
@@ -114,8 +173,44 @@ class FakeEngine:
         e0 = self.epoch
         self.epoch += n
         if hashes:
-            return np.array([self._share(e0 + k + 1) for k in range(n)], dtype=np.uint64)
+            return np.array([self._hash(e0 + k + 1) for k in range(n)], dtype=np.uint64)
         return None
+
+    def _my_rows(self, epoch):
+        return FakeBoard.words(self.board.rows(np.arange(self.row0, self.row0 + self.rows), epoch))
+
+    def snapshot(self, out=None):
+        d = self._my_rows(self.epoch)
+        if out is None:
+            return d
+        out[...] = d
+        return out
+
+    def checkpoint(self):
+        from gameoflife.elastic import checkpoint_buffer
+        blob, data = checkpoint_buffer(dict(width=self.w, height=self.h, row0=self.row0, epoch=self.epoch,
+                                            topology=0, birth=8, survive=12), self.rows, 2)
+        data[...] = self._my_rows(self.epoch)
+        log("checkpoint", f"{self.w}x{self.rows}", self.row0, self.epoch)
+        return blob
+
+    def restore(self, blob):
+        from gameoflife.elastic import parse_checkpoint
+        h, data = parse_checkpoint(bytes(blob))
+        if (h["width"], h["height"], h["row0"], h["rows"], h["wwords"]) != (self.w, self.h, self.row0, self.rows, 2):
+            raise ValueError(f"checkpoint {h} does not fit the context {self.row0}+{self.rows}")
+        if not np.array_equal(data, self._my_rows(h["epoch"])):
+            raise ValueError(f"checkpoint rows {self.row0}+{self.rows} at epoch {h['epoch']} are not the board's")
+        self.epoch = h["epoch"]
+        log("restore", f"{self.w}x{self.rows}", self.row0, self.epoch)
+
+    def replay(self, d, above, below):
+        up = FakeBoard.words(self.board.rows(np.arange(self.row0 - d, self.row0), self.epoch))
+        dn = FakeBoard.words(self.board.rows(np.arange(self.row0 + self.rows, self.row0 + self.rows + d), self.epoch))
+        if not (np.array_equal(above, up) and np.array_equal(below, dn)):
+            raise ValueError(f"light cone of rows {self.row0}+{self.rows} at epoch {self.epoch} is wrong")
+        log("replay", f"{self.w}x{self.rows}", self.row0, self.epoch, d)
+        return self.step(d, hashes=True)
 
     def sync(self):
         pass
@@ -150,6 +245,29 @@ class FakeEngine:
         return (12 if g > 8 else 16), 124
 
 
+# The gloo group standing in for the current RCCL ring: the job's world at
+# first; a later ring (the fault drill's survivors) gets a subgroup of the
+# ranks still in it.  Group creation is collective over the whole job, so
+# every rank -- the lost one included -- creates it: the lost rank does so
+# when it drops its context (comm_abort is the last call it makes).
+_GROUP = None
+
+
+def _join(rank, world):
+    global _GROUP
+    import torch.distributed as dist
+    full = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == full or world == 1 and full == 1:
+        _GROUP = None  # the default group
+        return
+    lost = _lost_rank(full)
+    _GROUP = dist.new_group([r for r in range(full) if r != lost])
+
+
+def _lost_rank(full):
+    return max(0, min(3, full - 1))
+
+
 def install():
     native = types.ModuleType("gameoflife._native")
     native.GOL_UNIQUE_ID_BYTES = 128
@@ -171,6 +289,9 @@ def install():
     engine.GolEngine = FakeEngine
     pkg = types.ModuleType("gameoflife")
     pkg._native, pkg.engine = native, engine
+    # the pure-Python modules (elastic: the fault drill's checkpoint files and
+    # light cones; shard) load from the real package, around the stand-ins
+    pkg.__path__ = [os.path.join(ROOT, "akka-game-of-life_amd", "gameoflife")]
     sys.modules.update({"gameoflife": pkg, "gameoflife._native": native, "gameoflife.engine": engine})
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:  # the stand-in for the engine's RCCL all-reduce

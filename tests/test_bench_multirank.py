@@ -40,7 +40,7 @@ def _run(world, tmp_path, *args, extra_env=None, rc=0):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_multirank_bench_line(tmp_path, world):
-    outs, logs = _run(world, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu")
+    outs, logs = _run(world, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-fault")
     lines = [ln for ln in outs[0].splitlines() if ln.strip()]
     assert len(lines) == 1, outs[0]
     assert all(not o.strip() for o in outs[1:])  # only rank 0 prints
@@ -169,7 +169,7 @@ def test_torchrun_launch_like_the_driver(tmp_path):
     env = dict(os.environ, FAKE_LOG_DIR=str(tmp_path), OMP_NUM_THREADS="1")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), RUNNER,
-                        "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu"],
+                        "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-cpu", "--no-fault"],
                        env=env, capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -177,3 +177,53 @@ def test_torchrun_launch_like_the_driver(tmp_path):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["parity"]["match"] is True
     assert sum(d["ranks"]["rows"]) == 262144
+
+
+@pytest.mark.parametrize("world", [3, 2, 5])
+def test_fault_drill_sub_line(tmp_path, world):
+    """configs[4] in the N > 1 bench: after the timed
+    windows the ranks re-run the board from the seed with checkpoint files
+    every 10 generations; rank min(3, N - 1) drops its context after
+    generation 25 of 50 (its process stays up and exits 0, printing
+    nothing); the rank above it restores the lost block's epoch-20 file,
+    takes the 5-row light cone from its neighbours' files, replays the block
+    alone and merges it with its own rows -- the fake engine refuses a blob,
+    a light cone or a merge holding any other rows than the board's at that
+    epoch -- and the N - 1 survivors join a new ring and step on to 50.
+    Every global hash (before, replayed, at the loss, after, final) equals
+    bench_262144.json, and the sub-line carries its parity and wall times."""
+    outs, logs = _run(world, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary")
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    assert all(not o.strip() for o in outs[1:])
+    f = d["fault_recovery"]
+    victim = min(3, world - 1)
+    host = victim - 1
+    assert f["world_after"] == world - 1 and f["checkpoint_epoch"] == 20 and f["replayed_generations"] == 5
+    assert f["parity"]["match"] is True and len(f["parity"]["checks"]) == 5
+    assert f["after"]["generations"] == 25 and f["after"]["value"] > 0 and f["recovery_ms"] >= 0
+    assert d["parity_ok"] is True and d["parity"]["match"] is True
+    whats = [c["what"] for c in d["parity"]["checks"] if c["what"].startswith("fault drill")]
+    assert len(whats) == 5
+    H = 262144
+    for r, log in enumerate(logs):
+        i_seed = max(i for i, ln in enumerate(log) if ln.startswith("seed 262144x"))
+        drill = log[i_seed:]
+        ev = [ln.split()[0] for ln in drill]
+        assert [ln.split()[3] for ln in drill if ln.startswith("checkpoint")] == ["10", "20"]
+        assert "comm_abort" in ev
+        if r == victim:  # drops everything after generation 25: no further step, ring or hash
+            i_abort = ev.index("comm_abort")
+            assert ev[i_abort + 1:] == ["close"], drill[i_abort:]
+            continue
+        comm = [ln.split() for ln in drill if ln.startswith("comm_init")]
+        assert [c[2:] for c in comm] == [[str(r if r < victim else r - 1), str(world - 1)]]
+        if r == host:
+            v0 = victim * (H // world) + min(victim, H % world)
+            vn = H // world + (1 if victim < H % world else 0)
+            assert f"restore 262144x{vn} {v0} 20" in drill and f"replay 262144x{vn} {v0} 20 5" in drill
+            mine = H // world + (1 if host < H % world else 0)
+            assert any(ln.startswith(f"create 262144x{mine + vn} ") for ln in drill)
+            assert any(ln.startswith(f"restore 262144x{mine + vn} ") and ln.endswith(" 25") for ln in drill)
+        steps = [ln.split()[2] for ln in drill if ln.startswith("step 262144x") and "x%d " % vn not in ln] \
+            if r == host else [ln.split()[2] for ln in drill if ln.startswith("step 262144x")]
+        assert steps[-1] == "25"

@@ -95,3 +95,46 @@ def test_torchrun_key_names_the_agent(monkeypatch):
     monkeypatch.setattr(os, "getppid", lambda: 1)
     other_agent = job.uid_path()
     assert len({plain, here, other_agent}) == 3
+
+
+def test_launch_key_outside_torchrun(monkeypatch):
+    """Outside torch.distributed.run the key carries the ranks' common parent
+    too (address + port alone let a crashed earlier job's file be
+    read), or GOL_BENCH_RUN_ID when the launcher names the launch; a later
+    ring of the same job (the fault drill's) has its own file."""
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    monkeypatch.delenv("GOL_BENCH_RUN_ID", raising=False)
+    job = _job(monkeypatch, 1, 41011)
+    here = job.uid_path()
+    assert job.uid_path("fault") != here
+    monkeypatch.setattr(os, "getppid", lambda: 1)
+    other_parent = job.uid_path()
+    monkeypatch.setenv("GOL_BENCH_RUN_ID", "launch-a")
+    a = job.uid_path()
+    monkeypatch.setattr(os, "getppid", lambda: 2)
+    assert job.uid_path() == a  # an explicit launch id does not depend on the parent
+    monkeypatch.setenv("GOL_BENCH_RUN_ID", "launch-b")
+    assert len({here, other_parent, a, job.uid_path()}) == 4
+
+
+def test_multi_node_launch_fails_fast(monkeypatch):
+    """The file rendezvous serves one node: WORLD_SIZE > LOCAL_WORLD_SIZE
+    stops with a message instead of waiting for a file no other node sees."""
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    try:
+        _job(monkeypatch, 0, 41012)
+    except SystemExit as e:
+        assert "one node" in str(e)
+    else:
+        raise AssertionError("a 2-node launch was accepted")
+
+
+def test_later_ring_joins_with_its_own_rank(monkeypatch):
+    """join(tag=..., rank=..., world=...): the fault drill's N - 1 ring, with
+    the survivors renumbered; the job's own engine is left alone."""
+    job = _job(monkeypatch, 0, 41013)
+    first, later = _Eng(), _Eng()
+    job.join(first, _N)
+    job.join(later, _N, tag="fault", rank=0, world=1)
+    assert later.joined == (bytes(range(128)), 0, 1) and later.reduced == 0  # a 1-rank ring needs no barrier
+    assert job.eng is first
