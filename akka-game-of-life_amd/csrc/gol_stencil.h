@@ -1137,6 +1137,10 @@ __device__ __forceinline__ void pend_issue(const Words<2>& w, int addr_l, int ad
     pd.o = w.w[1];
     pd.l = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_l, (int)w.w[1]);
     pd.r = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_r, (int)w.w[0]);
+    // keep the requests where the row is made: left to itself the scheduler
+    // sinks them to the end of the step and pulls their uses to its start,
+    // leaving ~50 instructions of latency cover instead of a whole step
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // arrive() on a pair row whose neighbour words came over the crossbar.
@@ -1153,7 +1157,7 @@ __device__ __forceinline__ void pend_arrive(const PendRow& pd, HRow<2, false>& o
 }
 
 template <int G>
-__global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_bp_kernel(const StepParams p) {
+__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, 3) void multistep_bp_kernel(const StepParams p) {
     constexpr int VEC = 2;
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     constexpr int kOut = (kWaveLanes - 2) * VEC;
@@ -1199,7 +1203,29 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_bp_kernel(c
 #pragma unroll
         for (int k = 0; k < kMRing; ++k) in[k].w[0] = in[k].w[1] = 0u;
 
-        auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(row_ptr(p, brow(m), G), lcol, d); };
+        // row_ptr without selects between two argument fields: the compiler
+        // folds such a select of two loads into one load from a selected
+        // address -- an s_load per stream row -- and scalar loads return out
+        // of order, so each wait for one is an lgkmcnt(0) that also drains
+        // the ds_bpermute in flight.  Offsets and deltas computed once are
+        // values, not loads.
+        const uint32_t* const cur = p.cur;
+        const int64_t pitch = p.pitch;
+        const int64_t d_top = p.halo_top - p.cur, d_bot = p.halo_bot - p.cur;
+        const int64_t d_stride = p.halo_stride - p.pitch;
+        const int lrows = p.rows, wrap_y = p.wrap_y;
+        auto rowp = [&](int r) -> const uint32_t* {
+            const bool top = r < 0, bot = r >= lrows;
+            int w = top ? r + lrows : (bot ? r - lrows : r);
+            if (wrap_y && lrows < G) {
+                w = r % lrows;
+                w = w < 0 ? w + lrows : w;
+            }
+            const bool halo = !wrap_y && (top || bot);
+            const int64_t idx = halo ? (top ? r + G : r - lrows) : (wrap_y ? w : r);
+            return cur + (halo ? (top ? d_top : d_bot) : 0) + idx * (pitch + (halo ? d_stride : 0));
+        };
+        auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(rowp(brow(m)), lcol, d); };
         auto slot3 = [](int x) { return ((x % 3) + 3) % 3; };
 
         // Step q (ring slot u = q % kMRing): prefetch input row q + kHgPF;

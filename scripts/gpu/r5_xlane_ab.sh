@@ -6,7 +6,7 @@
 # same box, interleaved.  Parity first: the bp kernel suite and the fault drill.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-mkdir -p gpurun_out/xlane
+rm -rf gpurun_out/xlane; mkdir -p gpurun_out/xlane
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_xlane.py tests/test_gpu_fault_drill.py > gpurun_out/xlane/parity.txt 2>&1 || { tail -40 gpurun_out/xlane/parity.txt; exit 1; }
 tail -2 gpurun_out/xlane/parity.txt
 B="python3 bench.py --steps 20 --warmup 5 --no-secondary --no-ring --no-cpu"
@@ -14,12 +14,12 @@ for r in 1 2 3; do
   timeout -k 10 200 $B > gpurun_out/xlane/dpp_plan_$r.json 2>/dev/null || exit 1
   GOL_XLANE=lds timeout -k 10 200 $B --gpp 7 > gpurun_out/xlane/lds_g7_$r.json 2>/dev/null || exit 1
   timeout -k 10 200 $B --gpp 7 > gpurun_out/xlane/dpp_g7_$r.json 2>/dev/null || exit 1
-  GOL_XLANE=lds timeout -k 10 200 $B --gpp 6 > gpurun_out/xlane/lds_g6_$r.json 2>/dev/null || exit 1
+  GOL_XLANE=lds timeout -k 10 200 $B --gpp 8 > gpurun_out/xlane/lds_g8_$r.json 2>/dev/null || exit 1
   echo "round $r done"
 done
 python3 - <<'PY'
 import json, glob
-for k in ("dpp_plan", "lds_g7", "dpp_g7", "lds_g6"):
+for k in ("dpp_plan", "lds_g7", "dpp_g7", "lds_g8"):
     vals = []
     for f in sorted(glob.glob(f"gpurun_out/xlane/{k}_*.json")):
         d = json.load(open(f))
