@@ -361,18 +361,6 @@ int device_ilv(int32_t topology, int64_t wwords) {
 
 constexpr int kDefaultXcdChunk = 8;
 
-// Cross-lane words of the pair B3/S23 torus passes: DPP wave shifts (0,
-// multistep_hg_kernel) or ds_bpermute one step ahead (1, multistep_bp_kernel;
-// GOL_XLANE=lds).  Same-box A/B switch of VERDICT r04 item 2's experiment; the
-// results are identical either way.
-int xlane_env() {
-    static const int v = [] {
-        const char* e = getenv("GOL_XLANE");
-        return (e && strcmp(e, "lds") == 0) ? 1 : 0;
-    }();
-    return v;
-}
-
 // Blocks per XCD chunk of the step kernels' block order (gol_stencil.h
 // xcd_block).  GOL_XCD_CHUNK overrides (A/B experiments; 1 = dispatch order).
 int xcd_chunk_env() {  // 0: not set
@@ -627,7 +615,6 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.birth = ctx->birth;
     p.survive = ctx->survive;
     p.xcd_chunk = xcd_chunk(gens, p.strips);
-    p.xlane = (xlane_env() && vec == 2 && ctx->ilv == 2 && life && slots == nullptr && gens > 1) ? 1 : 0;
     const int gx = (int)((waves + gol::kWavesPerWG - 1) / gol::kWavesPerWG);
     EventPair* ev = nullptr;
     p.clk = nullptr;

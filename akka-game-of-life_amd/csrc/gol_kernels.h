@@ -101,7 +101,6 @@ struct StepParams {
     uint32_t birth;
     uint32_t survive;
     int32_t xcd_chunk;         // consecutive blocks kept on one XCD (gol_stencil.h xcd_block; <= 1: off)
-    int32_t xlane;             // pair B3/S23 torus passes: 1 = neighbour words over ds_bpermute (multistep_bp_kernel)
     unsigned long long* clk;   // launch clock probe slot (kClockSlotWords u64), or null (gol_stencil.h clock_probe_*)
 };
 

@@ -1109,179 +1109,6 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
     clock_probe_end(p.clk, clk0);
 }
 
-// --------------------------------------------------------------------------
-// G generations per pass, horizontal-first, cross-lane words over the LDS
-// crossbar (VERDICT r04 item 2's experiment; B3/S23 torus, pair lanes,
-// unhashed).
-//
-// multistep_hg_kernel moves the two words a pair lane needs from its
-// neighbours (the previous lane's odd word, the next lane's even word) with
-// two DPP wave shifts per arriving row: VALU instructions at half the issue
-// rate of v_bitop3, 8.6 of the loop's 26.8 issue cycles per word-generation
-// with the funnel shift.  Here they travel by ds_bpermute on the LDS pipe.
-// Its latency (~100+ cycles) is hidden by delaying every row's arrival (the
-// horizontal sums) by one stream step: a row produced at step q issues its
-// two ds_bpermute and arrives at step q + 1, after the whole step's other
-// work.  So stage s produces stream row q - 2s at step q (one step later per
-// stage than multistep_hg_kernel), a pass takes n_in + G steps, and every
-// stage holds one row in flight (its two words and the two neighbour words:
-// +4 VGPRs per stage).
-// --------------------------------------------------------------------------
-struct PendRow {
-    uint32_t e, o;  // the row's pair words
-    uint32_t l, r;  // the previous lane's odd word, the next lane's even word (ds_bpermute results)
-};
-
-__device__ __forceinline__ void pend_issue(const Words<2>& w, int addr_l, int addr_r, PendRow& pd) {
-    pd.e = w.w[0];
-    pd.o = w.w[1];
-    pd.l = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_l, (int)w.w[1]);
-    pd.r = (uint32_t)__builtin_amdgcn_ds_bpermute(addr_r, (int)w.w[0]);
-    // keep the requests where the row is made: left to itself the scheduler
-    // sinks them to the end of the step and pulls their uses to its start,
-    // leaving ~50 instructions of latency cover instead of a whole step
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// arrive() on a pair row whose neighbour words came over the crossbar.
-__device__ __forceinline__ void pend_arrive(const PendRow& pd, HRow<2, false>& o) {
-    const uint32_t rv[2] = {pd.e, pd.o};
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        uint32_t w, e;
-        neighbours<2>(rv, pd.l, pd.r, j, w, e);
-        o.h0[j] = GOL_BITOP3(w, rv[j], e, kXor3);
-        o.h1[j] = GOL_BITOP3(w, rv[j], e, kMaj);
-        o.r[j] = rv[j];
-    }
-}
-
-template <int G>
-__global__ __launch_bounds__(kWaveLanes* kWavesPerWG, 3) void multistep_bp_kernel(const StepParams p) {
-    constexpr int VEC = 2;
-    static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
-    constexpr int kOut = (kWaveLanes - 2) * VEC;
-    const int lane = threadIdx.x & (kWaveLanes - 1);
-    const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
-    const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
-    const ClockStart clk0 = clock_probe_begin(p.clk);
-    const int rg = tile.range, strip = tile.strip, bandi = tile.band;
-    if (bandi < p.nbands[rg]) {
-        const int r_begin = p.row_lo[rg] + bandi * p.band[rg];
-        const int r_end = min(r_begin + p.band[rg], p.row_hi[rg]);
-        const int nrows = r_end - r_begin;
-        const int n_in = nrows + 2 * G;
-        const int s0 = strip * kOut;
-        const int nout = min(kOut, p.wwords - s0);
-        const int col = s0 + (lane - 1) * VEC;
-        const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
-        // idle lanes off (multistep_hg_kernel): the right halo lane then reads
-        // a switched-off lane's word -- garbage in its outermost bit, as at
-        // the wave's ends (lane 0 reads lane 63's)
-        if (lane > (nout + VEC - 1) / VEC + 1) return;
-        int lcol = col % p.wwords;
-        if (lcol < 0) lcol += p.wwords;
-        const int addr_l = ((lane + kWaveLanes - 1) & (kWaveLanes - 1)) * 4;
-        const int addr_r = ((lane + 1) & (kWaveLanes - 1)) * 4;
-        const bool up = (bandi & 1) != 0;
-        auto brow = [&](int m) -> int { return up ? r_end - 1 + G - m : r_begin - G + m; };
-
-        Words<VEC> in[kMRing];
-        HRow<VEC, false> hr[G][3];  // ring s: arrivals of stage-s rows (stage 0 = input), slot = row % 3
-        PairSum<VEC> pst[G];        // stage s's last even-row P
-        PendRow pend[G];            // stage s's row in flight (stage 0: the input row)
-#pragma unroll
-        for (int s = 0; s < G; ++s) {
-            pend[s].e = pend[s].o = pend[s].l = pend[s].r = 0u;
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) pst[s].p0[j] = pst[s].p1[j] = pst[s].p2[j] = 0u;
-#pragma unroll
-            for (int k = 0; k < 3; ++k)
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) hr[s][k].h0[j] = hr[s][k].h1[j] = hr[s][k].r[j] = 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kMRing; ++k) in[k].w[0] = in[k].w[1] = 0u;
-
-        // row_ptr without selects between two argument fields: the compiler
-        // folds such a select of two loads into one load from a selected
-        // address -- an s_load per stream row -- and scalar loads return out
-        // of order, so each wait for one is an lgkmcnt(0) that also drains
-        // the ds_bpermute in flight.  Offsets and deltas computed once are
-        // values, not loads.
-        const uint32_t* const cur = p.cur;
-        const int64_t pitch = p.pitch;
-        const int64_t d_top = p.halo_top - p.cur, d_bot = p.halo_bot - p.cur;
-        const int64_t d_stride = p.halo_stride - p.pitch;
-        const int lrows = p.rows, wrap_y = p.wrap_y;
-        auto rowp = [&](int r) -> const uint32_t* {
-            const bool top = r < 0, bot = r >= lrows;
-            int w = top ? r + lrows : (bot ? r - lrows : r);
-            if (wrap_y && lrows < G) {
-                w = r % lrows;
-                w = w < 0 ? w + lrows : w;
-            }
-            const bool halo = !wrap_y && (top || bot);
-            const int64_t idx = halo ? (top ? r + G : r - lrows) : (wrap_y ? w : r);
-            return cur + (halo ? (top ? d_top : d_bot) : 0) + idx * (pitch + (halo ? d_stride : 0));
-        };
-        auto load_m = [&](int m, Words<VEC>& d) { load_words<VEC>(rowp(brow(m)), lcol, d); };
-        auto slot3 = [](int x) { return ((x % 3) + 3) % 3; };
-
-        // Step q (ring slot u = q % kMRing): prefetch input row q + kHgPF;
-        // input row q - 1 arrives and row q's neighbour words are requested;
-        // stage s computes stream row m = q - 2s from ring s-1 rows m-1, m,
-        // m+1 (m+1 arrived this step), then its row m-1 (computed at step
-        // q - 1) arrives and row m's neighbour words are requested.  Stage s
-        // has valid rows from m = s on (q = 3s); a paired stage also runs the
-        // step before, to form that row's P when it is odd.
-        auto row_step = [&](const int q, const int u, const bool fill) __attribute__((always_inline)) {
-            load_m(min(q + kHgPF, n_in - 1), in[(u + kHgPF) % kMRing]);
-            pend_arrive(pend[0], hr[0][slot3(u - 1)]);
-            pend_issue(in[u], addr_l, addr_r, pend[0]);
-#pragma unroll
-            for (int s = 1; s <= G; ++s) {
-                if (fill && q < 3 * s - 1) break;
-                const int m = q - 2 * s;
-                Words<VEC> o;
-                const HRow<VEC, false>& A = hr[s - 1][slot3(u - 2 * s - 1)];
-                const HRow<VEC, false>& C = hr[s - 1][slot3(u - 2 * s)];
-                const HRow<VEC, false>& B = hr[s - 1][slot3(u - 2 * s + 1)];
-                // q - u is a multiple of kMRing (even): m's parity is u's
-                if ((u & 1) == 0) {
-                    pair_sum<VEC>(C.h0, C.h1, B.h0, B.h1, pst[s - 1]);  // h(m) + h(m + 1)
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j)
-                        o.w[j] = rule_b3s23_pair(pst[s - 1].p0[j], pst[s - 1].p1[j], pst[s - 1].p2[j], A.h0[j],
-                                                 A.h1[j], C.r[j]);
-                } else {  // h(m - 1) + h(m), formed by the even row before
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j)
-                        o.w[j] = rule_b3s23_pair(pst[s - 1].p0[j], pst[s - 1].p1[j], pst[s - 1].p2[j], B.h0[j],
-                                                 B.h1[j], C.r[j]);
-                }
-                if (s < G) {
-                    pend_arrive(pend[s], hr[s][slot3(u - 2 * s - 1)]);
-                    pend_issue(o, addr_l, addr_r, pend[s]);
-                } else {
-                    const bool own_row = m >= G && m < n_in - G;
-                    store_row<VEC>(p.nxt + (int64_t)brow(m) * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
-                }
-            }
-        };
-
-#pragma unroll
-        for (int t = 0; t < kHgPF; ++t) load_m(min(t, n_in - 1), in[t]);
-        constexpr int kFill = (3 * G + kMRing - 1) / kMRing * kMRing;  // whole ring turns
-        static_for<kFill>([&](auto Q) __attribute__((always_inline)) { row_step(Q.value, Q.value % kMRing, true); });
-        for (int q0 = kFill; q0 < n_in + G; q0 += kMRing) {
-#pragma unroll
-            for (int u = 0; u < kMRing; ++u) row_step(q0 + u, u, false);
-        }
-    }
-    clock_probe_end(p.clk, clk0);
-}
-
 // The horizontal-first kernel keeps three planes per ring row: at 16-byte
 // lanes it needs 183-270 registers or spills (1-1.6 KB scratch per lane), so
 // VEC = 4 (gol_set_tuning's words_per_lane = 4) runs the vertical-first
@@ -1299,9 +1126,6 @@ hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     } else if constexpr (!kBuilt<VEC, G, LIFE, CLIPPED>) {
         return hipErrorInvalidValue;
     } else if constexpr (VEC <= 2) {
-        if constexpr (VEC == 2 && ILV == 2 && LIFE && !HASH && !CLIPPED) {
-            if (p.xlane == 1) return launch_kernel(multistep_bp_kernel<G>, grid, block, st, p);
-        }
         return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     } else {
         return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);

@@ -11,7 +11,7 @@ import re
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # GOL_LIB_PATH: an alternative build of the same library, for A/B timing
-# experiments only (scripts/ab_build.sh); products use the in-tree build.
+# experiments only (scripts/archive/ab_build.sh); products use the in-tree build.
 LIB_PATH = os.environ.get("GOL_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libgol.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "gol.h")
 

@@ -25,6 +25,16 @@ constexpr int kIters = 4096;
 //           arrive (per row 2 DPP + 2 v_alignbit + 4 v_bitop3), their P is formed
 //           per word (v_xor + v_and + 2 v_bitop3) and each of the 2 x 2 words
 //           runs the 4-v_bitop3 tail: 40 VALU per 4 word-generations.
+// Round 5: the fused hash's price on MODE 8's mix.
+//   MODE 9:  today's hash -- per output row and pair two v_mad_u64_u32 (the
+//            even and odd word by their row keys, summed) and one ds_add_u64
+//            (no return) into the lane's LDS sum of that generation.
+//   MODE 10: the same two v_mad_u64_u32 per row, summed in registers (no
+//            LDS): what register sums would save (+2 VGPRs per stage in the
+//            kernel).
+//   MODE 11: a "full-rate" hash for comparison: one v_dot4_u32_u8 per word
+//            (bytes by 8-bit keys into a 32-bit sum) -- a weaker hash, priced
+//            only to bound what any multiply-free scheme could gain.
 __device__ __forceinline__ uint32_t rule7(uint32_t a0, uint32_t a1, uint32_t c0, uint32_t c1, uint32_t b0, uint32_t b1,
                                           uint32_t alive) {
     const uint32_t e1 = __builtin_amdgcn_bitop3_b32(a0, c0, b0, 0x69);
@@ -39,12 +49,18 @@ __device__ __forceinline__ uint32_t rule7(uint32_t a0, uint32_t a1, uint32_t c0,
 template <int MODE, int CH>
 __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned long long* clk) {
     uint32_t a[CH], b[CH], c[CH], d[CH], pl[CH], pr[CH];
+    unsigned long long hs[CH];
+    uint32_t hs32[CH];
+    __shared__ unsigned long long hsum_all[4 * 2 * 64];
     const int lane = threadIdx.x & 63;
+    unsigned long long* hsum = hsum_all + (threadIdx.x >> 6) * 128;
+    hsum[lane] = hsum[64 + lane] = 0;
     const int addr_l = ((lane + 63) & 63) * 4, addr_r = ((lane + 1) & 63) * 4;  // ds_bpermute byte addresses
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
         a[i] = seed * (threadIdx.x + i); b[i] = a[i] ^ 0x9e3779b9u; c[i] = a[i] + 17u; d[i] = b[i] * 5u;
         pl[i] = a[i] >> 3; pr[i] = b[i] << 3;
+        hs[i] = 0; hs32[i] = 0;
     }
     unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     for (int it = 0; it < kIters; ++it) {
@@ -160,6 +176,55 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
                 }
                 c[i] = hh0[1][0]; pl[i] = hh0[0][1]; pr[i] = hh1[1][1];
                 a[i] = out4[0][0]; b[i] = out4[0][1]; d[i] = out4[1][0] ^ out4[1][1];
+            } else if constexpr (MODE == 9 || MODE == 10 || MODE == 11) {
+                uint32_t hh0[2][2], hh1[2][2], rr[2][2];
+                uint32_t rows[2][2] = {{a[i], b[i]}, {d[i], c[i] ^ a[i]}};
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t e = rows[r][0], o = rows[r][1];
+                    const uint32_t left = (uint32_t)__builtin_amdgcn_mov_dpp((int)o, 0x138, 0xf, 0xf, true);
+                    const uint32_t right = (uint32_t)__builtin_amdgcn_mov_dpp((int)e, 0x130, 0xf, 0xf, true);
+                    const uint32_t we = __builtin_amdgcn_alignbit(o, left, 31);
+                    const uint32_t eo = __builtin_amdgcn_alignbit(right, e, 1);
+                    hh0[r][0] = __builtin_amdgcn_bitop3_b32(we, e, o, 0x96);
+                    hh1[r][0] = __builtin_amdgcn_bitop3_b32(we, e, o, 0xe8);
+                    hh0[r][1] = __builtin_amdgcn_bitop3_b32(e, o, eo, 0x96);
+                    hh1[r][1] = __builtin_amdgcn_bitop3_b32(e, o, eo, 0xe8);
+                    rr[r][0] = e; rr[r][1] = o;
+                }
+                uint32_t out4[2][2];
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint32_t k = hh0[0][j] & hh0[1][j];
+                    const uint32_t p0 = hh0[0][j] ^ hh0[1][j];
+                    const uint32_t p1 = __builtin_amdgcn_bitop3_b32(hh1[0][j], hh1[1][j], k, 0x96);
+                    const uint32_t p2 = __builtin_amdgcn_bitop3_b32(hh1[0][j], hh1[1][j], k, 0xe8);
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const uint32_t x0 = r ? pl[i] : c[i], x1 = r ? pr[i] : (c[i] ^ 0x5a5a5a5au), al = rr[r][j];
+                        const uint32_t g1 = __builtin_amdgcn_bitop3_b32(p0, x0, al, 0x43);
+                        const uint32_t g2 = __builtin_amdgcn_bitop3_b32(p1, p2, g1, 0x18);
+                        const uint32_t g3 = __builtin_amdgcn_bitop3_b32(p2, x1, g2, 0x26);
+                        out4[r][j] = __builtin_amdgcn_bitop3_b32(g3, al, g1, 0xd0);
+                    }
+                }
+                // the hash of the two output rows (row keys: wave-uniform, per chain)
+                const uint32_t ka = 0x9E3779B1u * (uint32_t)(it + i) | 1u, kb = ka + 0x6A09E666u;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    if constexpr (MODE == 11) {
+                        hs32[i] = __builtin_amdgcn_udot4(out4[r][0], ka, hs32[i], false);
+                        hs32[i] = __builtin_amdgcn_udot4(out4[r][1], kb, hs32[i], false);
+                    } else {
+                        unsigned long long t = (unsigned long long)out4[r][0] * ka;
+                        t += (unsigned long long)out4[r][1] * kb;
+                        if constexpr (MODE == 9) __hip_atomic_fetch_add(&hsum[r * 64 + lane], t, __ATOMIC_RELAXED,
+                                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else hs[i] += t;
+                    }
+                }
+                c[i] = hh0[1][0]; pl[i] = hh0[0][1]; pr[i] = hh1[1][1];
+                a[i] = out4[0][0]; b[i] = out4[0][1]; d[i] = out4[1][0] ^ out4[1][1];
             } else {  // step-kernel mix: 1 DPP, 2 alignbit, 9 bitop3, 1 xor  (13)
                 const uint32_t l = (uint32_t)__builtin_amdgcn_mov_dpp((int)c[i], 0x138, 0xf, 0xf, true);
                 const uint32_t w = __builtin_amdgcn_alignbit(a[i], l, 31);
@@ -181,7 +246,9 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed, unsigned 
     unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t acc = 0;
 #pragma unroll
-    for (int i = 0; i < CH; ++i) acc ^= a[i] ^ b[i] ^ c[i] ^ d[i] ^ pl[i] ^ pr[i];
+    for (int i = 0; i < CH; ++i) acc ^= a[i] ^ b[i] ^ c[i] ^ d[i] ^ pl[i] ^ pr[i] ^ (uint32_t)hs[i] ^ (uint32_t)(hs[i] >> 32) ^ hs32[i];
+    __syncthreads();
+    acc ^= (uint32_t)hsum[lane] ^ (uint32_t)(hsum[64 + lane] >> 32);
     out[blockIdx.x * 256 + threadIdx.x] = acc;
     if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
 }
@@ -228,6 +295,22 @@ int main() {
             run<4, 4>("per-row circuit (22 VALU/pair)", 22, w, out, clk, cus, 2);
             run<8, 1>("pair-row circuit (40 VALU/2 pairs)", 40, w, out, clk, cus, 4);
             run<8, 2>("pair-row circuit (40 VALU/2 pairs)", 40, w, out, clk, cus, 4);
+        }
+        return 0;
+    }
+    if (getenv("VALU_RATE_HASH")) {
+        // the pair-row mix (MODE 8, 40 VALU per 4 word-generations) unhashed,
+        // with today's hash (+4 v_mad_u64_u32 + 2 ds_add_u64), with register
+        // sums (+4 v_mad_u64_u32), and with a byte-dot hash (+4 v_dot4)
+        for (int w : {2, 3, 4}) {
+            run<8, 1>("pair-row, no hash", 40, w, out, clk, cus, 4);
+            run<8, 2>("pair-row, no hash", 40, w, out, clk, cus, 4);
+            run<9, 1>("pair-row, mad_u64 + ds_add", 44, w, out, clk, cus, 4);
+            run<9, 2>("pair-row, mad_u64 + ds_add", 44, w, out, clk, cus, 4);
+            run<10, 1>("pair-row, mad_u64 regs", 44, w, out, clk, cus, 4);
+            run<10, 2>("pair-row, mad_u64 regs", 44, w, out, clk, cus, 4);
+            run<11, 1>("pair-row, dot4 (weaker)", 44, w, out, clk, cus, 4);
+            run<11, 2>("pair-row, dot4 (weaker)", 44, w, out, clk, cus, 4);
         }
         return 0;
     }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/gpu_stall_pmc.sh (gpurun_out/stall): per config, the
+"""Summarise scripts/archive/gpu_stall_pmc.sh (gpurun_out/stall): per config, the
 fractions of wave-cycles parked on s_waitcnt (SQ_WAIT_ANY), stalled at issue
 (SQ_WAIT_INST_ANY) and issuing (SQ_ACTIVE_INST_ANY / _VALU), over the
 largest-grid step-kernel launches (warm-up pass dropped).
