@@ -147,6 +147,9 @@ class FakeEngine:
 
     def comm_init(self, uid, rank, world):
         log("comm_init", uid.hex()[:16], rank, world)
+        if os.environ.get("FAKE_HANG_REJOIN") and world < int(os.environ.get("WORLD_SIZE", "1")):
+            import time
+            time.sleep(600)  # a ring rebuild that never completes (the drill's watchdog must end it)
         _join(rank, world)
 
     def comm_abort(self):
