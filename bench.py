@@ -685,7 +685,26 @@ def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     import shutil
     import numpy as np
     from gameoflife.elastic import ring_fault_drill
-    ckpt = job.uid_path("fault_ckpt") + "_dir"  # one node: the ranks share the temp directory
+    # The checkpoint files: every rank's shard, two epochs at the peak (a new
+    # file is written before the previous one is removed) -- twice the board.
+    # The first candidate directory with room for them (the same list on
+    # every rank of the node); rank 0's choice is all-reduced so all agree.
+    need = 2 * W * H // 8 + (1 << 30)
+    cands = [d for d in (os.environ.get("GOL_BENCH_CKPT_DIR"), tempfile.gettempdir(), "/dev/shm") if d]
+    pick = 0
+    if job.rank == 0:
+        for k, d in enumerate(cands):
+            try:
+                if shutil.disk_usage(d).free >= need:
+                    pick = k + 1
+                    break
+            except OSError:
+                pass
+    pick = int(eng.allreduce_u64(np.array([pick], dtype=np.uint64))[0])
+    if pick == 0:
+        return ({"status": "skipped", "reason": f"no directory among {cands} has {need / 2**30:.0f} GiB free "
+                 "for the checkpoint files"} if job.rank == 0 else None), eng
+    ckpt = os.path.join(cands[pick - 1], os.path.basename(job.uid_path("fault_ckpt")) + "_dir")
     if job.rank == 0:
         shutil.rmtree(ckpt, ignore_errors=True)
         os.makedirs(ckpt)
@@ -693,8 +712,15 @@ def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     make = lambda r0, n: GolEngine(W, H, topology="torus", rule="life", device=local, row0=r0, rows=n)  # noqa: E731
     join = lambda e, tag, r, w: job.join(e, N, tag=tag, rank=r, world=w)  # noqa: E731
     t0 = time.perf_counter()
-    eng, rep = ring_fault_drill(eng, make, join, job.rank, job.world, W, H, ckpt, seed=GOLDEN_SEED, victim=3,
-                                kill_at=25, gens=50, every=10)
+    try:
+        eng, rep = ring_fault_drill(eng, make, join, job.rank, job.world, W, H, ckpt, seed=GOLDEN_SEED, victim=3,
+                                    kill_at=25, gens=50, every=10)
+    except Exception as exc:  # noqa: BLE001 -- reported on the line; peers left in a collective meet the watchdog
+        parity.checks.append({"what": "fault drill", "board": f"{W}x{H}", "error": repr(exc), "match": False})
+        print(f"bench.py rank {job.rank}: fault drill failed: {exc!r}", file=sys.stderr, flush=True)
+        if job.rank == 0:
+            shutil.rmtree(ckpt, ignore_errors=True)
+        return ({"status": "error", "error": repr(exc)} if job.rank == 0 else None), None
     if eng is None:  # the lost rank: its context is gone, it sits out the rest
         return None, None
     nw, nr = rep["world_after"], job.rank if job.rank < rep["victim_rank"] else job.rank - 1
@@ -723,6 +749,7 @@ def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     after_gens = rep["generations"] - k
     ms = [c_.get("match") for c_ in checks]
     return {
+        "status": "ok",
         "workload": f"{W}x{H} torus B3/S23 over {job.world} ranks: rank {rep['victim_rank']} lost after generation "
                     f"{k} of {rep['generations']} (BASELINE.json configs[4]), its shard re-spawned on rank "
                     f"{rep['host_rank']}'s GPU, {nw} ranks after",

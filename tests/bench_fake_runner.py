@@ -190,6 +190,8 @@ class FakeEngine:
         return out
 
     def checkpoint(self):
+        if os.environ.get("FAKE_DRILL_RAISE") == str(RANK) and self.epoch == 20:
+            raise OSError(28, "No space left on device")  # a checkpoint write that fails mid-drill
         from gameoflife.elastic import checkpoint_buffer
         blob, data = checkpoint_buffer(dict(width=self.w, height=self.h, row0=self.row0, epoch=self.epoch,
                                             topology=0, birth=8, survive=12), self.rows, 2)
@@ -310,6 +312,9 @@ def install():
 
 
 if __name__ == "__main__":
+    if os.environ.get("FAKE_NO_ROOM"):  # no directory has room for the fault drill's checkpoint files
+        import shutil
+        shutil.disk_usage = lambda d: types.SimpleNamespace(total=1 << 30, used=1 << 30, free=0)
     install()
     sys.path.insert(0, ROOT)
     import bench

@@ -33,8 +33,8 @@ def _run(world, tmp_path, *args, extra_env=None, rc=0):
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=120) for p in procs]
     for r, (p, (o, e)) in enumerate(zip(procs, outs)):
-        if rc is None:  # the watchdog test: survivors stop with 4, the lost rank left with 0
-            assert p.returncode in (0, 4), e[-2000:]
+        if rc is None:  # the watchdog tests: stopped ranks exit 4, a failed drill 3, the lost rank 0
+            assert p.returncode in (0, 3, 4), e[-2000:]
         else:
             assert p.returncode == rc, e[-2000:]
     logs = [open(tmp_path / f"rank{r}.log").read().splitlines() for r in range(world)]
@@ -199,6 +199,7 @@ def test_fault_drill_sub_line(tmp_path, world):
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert all(not o.strip() for o in outs[1:])
     f = d["fault_recovery"]
+    assert f["status"] == "ok"
     victim = min(3, world - 1)
     host = victim - 1
     assert f["world_after"] == world - 1 and f["checkpoint_epoch"] == 20 and f["replayed_generations"] == 5
@@ -242,3 +243,25 @@ def test_fault_drill_watchdog(tmp_path):
     assert d["value"] > 0 and d["parity"]["match"] is True  # the measured windows are intact
     assert d["fault_recovery"] == {"status": "timed out", "timeout_s": 8.0}
     assert d["parity_ok"] is False and any("fault drill" in f for f in d["parity_failed"])
+
+
+def test_fault_drill_skips_without_room(tmp_path):
+    """No directory with room for the checkpoint files: every rank skips the
+    drill together (rank 0 decides), the line says so, and the measured
+    windows stand (exit 0)."""
+    outs, logs = _run(2, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
+                      extra_env={"FAKE_NO_ROOM": "1"})
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    assert d["fault_recovery"]["status"] == "skipped" and d["parity_ok"] is True
+    assert not any(ln.startswith("comm_abort") for log in logs for ln in log)
+
+
+def test_fault_drill_error_on_rank0(tmp_path):
+    """A drill that fails on rank 0 (a checkpoint write raising) still gets
+    the measured line out: status error, parity_ok false, exit 3 on rank 0;
+    the peers, left waiting in a collective, stop at the watchdog (exit 4)."""
+    outs, _ = _run(3, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
+                   "--fault-timeout", "8", extra_env={"FAKE_DRILL_RAISE": "0"}, rc=None)
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    assert d["fault_recovery"]["status"] == "error" and "No space left" in d["fault_recovery"]["error"]
+    assert d["value"] > 0 and d["parity_ok"] is False
