@@ -48,7 +48,11 @@
 extern "C" {
 #endif
 
-#define GOL_ABI_VERSION 1
+/* 2 (round 5): the state hash became a function of the cells alone (see the
+ * header comment); the values of tori with an even word count are unchanged,
+ * those of row-major boards (clipped, odd word counts) differ from version 1.
+ * The entry points and structs are those of version 1. */
+#define GOL_ABI_VERSION 2
 
 /* Return codes. */
 #define GOL_OK 0

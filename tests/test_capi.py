@@ -26,7 +26,7 @@ def test_exports_every_header_symbol():
 
 
 def test_abi_version_and_errors():
-    assert N.lib.gol_abi_version() == 1
+    assert N.lib.gol_abi_version() == 2  # round 5: the canonical state hash
     for code in range(7):
         assert N.lib.gol_strerror(code)
     assert N.lib.gol_strerror(99) == b"unknown error"
