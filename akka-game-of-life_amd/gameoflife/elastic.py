@@ -198,17 +198,37 @@ def blob_rows(blobs, indices) -> np.ndarray:
 
 def checkpoint_rows(ckpt_dir: str, epoch: int, indices) -> np.ndarray:
     """Rows `indices` (global row numbers in [0, height)) of the board at
-    `epoch`, cut from whatever shard files hold them."""
+    `epoch`, cut from whatever shard files hold them.  Only the rows asked
+    for are read (a light cone is a few rows of a file that may hold a GiB):
+    each file's header, then one read per run of consecutive rows."""
     idx = np.asarray(list(indices), dtype=np.int64)
-    blobs = []
+    out, done = None, np.zeros(idx.size, dtype=bool)
     for f0, fn, path in _shard_files(ckpt_dir, epoch):
-        if ((idx >= f0) & (idx < f0 + fn)).any():
-            with open(path, "rb") as f:
-                blobs.append(f.read())
-    try:
-        return blob_rows(blobs, idx)
-    except ValueError as e:
-        raise FileNotFoundError(f"epoch {epoch}: {e}") from None
+        sel = np.nonzero((~done) & (idx >= f0) & (idx < f0 + fn))[0]
+        if sel.size == 0:
+            continue
+        with open(path, "rb") as f:
+            hdr = f.read(_HDR.size)
+            magic, _, _, row0, rows, wwords, _, _, _, _, _ = _HDR.unpack_from(hdr, 0)
+            if magic != _MAGIC or row0 != f0 or rows != fn:
+                raise ValueError(f"{path}: not the checkpoint its name says")
+            if out is None:
+                out = np.zeros((idx.size, wwords), dtype=np.uint32)
+            order = sel[np.argsort(idx[sel], kind="stable")]
+            k = 0
+            while k < order.size:  # runs of consecutive rows: one read each
+                j = k
+                while j + 1 < order.size and idx[order[j + 1]] == idx[order[j]] + 1:
+                    j += 1
+                r_lo = int(idx[order[k]])
+                f.seek(_HDR.size + (r_lo - f0) * wwords * 4)
+                data = np.frombuffer(f.read((j - k + 1) * wwords * 4), dtype=np.uint32).reshape(-1, wwords)
+                out[order[k:j + 1]] = data
+                k = j + 1
+        done[sel] = True
+    if out is None or not done.all():
+        raise FileNotFoundError(f"epoch {epoch}: checkpoints do not hold rows {idx[~done][:4].tolist()}...")
+    return out
 
 
 def assemble_checkpoint(ckpt_dir: str, epoch: int, row0: int, rows: int) -> bytes:
