@@ -63,16 +63,28 @@ _MAGIC = b"GOLCKPT1"
 
 # ----------------------------------------------------------- checkpoints
 
-def parse_checkpoint(blob: bytes) -> tuple[dict, np.ndarray]:
-    """Header fields and packed rows (rows x wwords) of a gol_checkpoint blob."""
+def _header(blob) -> dict:
+    if len(blob) < _HDR.size:
+        raise ValueError("not a libgol checkpoint")
     magic, width, height, row0, rows, wwords, epoch, topology, birth, survive, _ = \
         _HDR.unpack_from(blob, 0)
     if magic != _MAGIC:
         raise ValueError("not a libgol checkpoint")
-    h = dict(width=width, height=height, row0=row0, rows=rows, wwords=wwords, epoch=epoch,
-             topology=topology, birth=birth, survive=survive)
-    data = np.frombuffer(blob, dtype=np.uint32, count=rows * wwords, offset=_HDR.size)
-    return h, data.reshape(rows, wwords)
+    return dict(width=width, height=height, row0=row0, rows=rows, wwords=wwords, epoch=epoch,
+                topology=topology, birth=birth, survive=survive)
+
+
+def parse_checkpoint(blob: bytes) -> tuple[dict, np.ndarray]:
+    """Header fields and packed rows (rows x wwords) of a gol_checkpoint blob."""
+    h = _header(blob)
+    data = np.frombuffer(blob, dtype=np.uint32, count=h["rows"] * h["wwords"], offset=_HDR.size)
+    return h, data.reshape(h["rows"], h["wwords"])
+
+
+def read_checkpoint_header(path: str) -> dict:
+    """Header fields of a checkpoint file, without reading its rows."""
+    with open(path, "rb") as f:
+        return _header(f.read(_HDR.size))
 
 
 def make_checkpoint(h: dict, packed: np.ndarray) -> bytes:
@@ -208,10 +220,10 @@ def checkpoint_rows(ckpt_dir: str, epoch: int, indices) -> np.ndarray:
         if sel.size == 0:
             continue
         with open(path, "rb") as f:
-            hdr = f.read(_HDR.size)
-            magic, _, _, row0, rows, wwords, _, _, _, _, _ = _HDR.unpack_from(hdr, 0)
-            if magic != _MAGIC or row0 != f0 or rows != fn:
+            h = _header(f.read(_HDR.size))
+            if h["row0"] != f0 or h["rows"] != fn:
                 raise ValueError(f"{path}: not the checkpoint its name says")
+            wwords = h["wwords"]
             if out is None:
                 out = np.zeros((idx.size, wwords), dtype=np.uint32)
             order = sel[np.argsort(idx[sel], kind="stable")]
@@ -237,8 +249,7 @@ def assemble_checkpoint(ckpt_dir: str, epoch: int, row0: int, rows: int) -> byte
     files = _shard_files(ckpt_dir, epoch)
     if not files:
         raise FileNotFoundError(f"no checkpoint at epoch {epoch}")
-    with open(files[0][2], "rb") as f:
-        header, _ = parse_checkpoint(f.read())
+    header = read_checkpoint_header(files[0][2])
     packed = checkpoint_rows(ckpt_dir, epoch, range(row0, row0 + rows))
     return make_checkpoint(dict(header, row0=row0, rows=rows, epoch=epoch), packed)
 
@@ -268,8 +279,7 @@ def light_cone(ckpt_dir: str, epoch: int, row0: int, rows: int, depth: int, heig
     files = _shard_files(ckpt_dir, epoch)
     if not files:
         raise FileNotFoundError(f"no checkpoint at epoch {epoch}")
-    with open(files[0][2], "rb") as f:
-        wwords = parse_checkpoint(f.read())[0]["wwords"]
+    wwords = read_checkpoint_header(files[0][2])["wwords"]
     return light_cone_from(lambda idx: checkpoint_rows(ckpt_dir, epoch, idx), row0, rows, depth, height, torus,
                            wwords)
 

@@ -106,3 +106,20 @@ def test_fault_drill_loopback_65536_golden(gpu, tmp_path):
         golden = [int(x, 16) for x in json.load(f)["hashes"]]
     out, _ = _drill(S, S, 4, 0x5EED, str(tmp_path))
     _check(out, golden[1:51], 4, 3)
+
+
+def test_fault_drill_loopback_262144_golden(gpu, tmp_path):
+    """The bench's own N = 8 drill (configs[4] on configs[3]'s board): eight
+    ranks of 262144^2 (1 GiB shards), rank 3 lost after 25 of 50, every hash
+    against bench_262144.json.  The checkpoint files peak at two epochs of the
+    board (16 GiB); without that much room in the test's directory it skips."""
+    import shutil
+    S = 262144
+    if shutil.disk_usage(str(tmp_path)).free < 2 * S * S // 8 + (4 << 30):
+        pytest.skip("no room for two epochs of 262144^2 checkpoint files")
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "bench_262144.json")) as f:
+        golden = [int(x, 16) for x in json.load(f)["hashes"]]
+    out, _ = _drill(S, S, 8, 0x5EED, str(tmp_path))
+    _check(out, golden[1:51], 8, 3)
+    print("drill wall per survivor: recovery %.3f s, after %.3f s, checkpoints %.3f s" % max(
+        (rep["recovery_s"], rep["after_s"], rep["checkpoint_s"]) for e, rep in out if e is not None))
