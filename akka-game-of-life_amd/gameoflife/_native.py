@@ -195,11 +195,6 @@ def device_ilv(width: int, topology: int = GOL_TORUS) -> int:
     return 2 if ww % 2 == 0 else 1
 
 
-def pair_layout(width: int, topology: int = GOL_TORUS) -> bool:
-    """True when libgol keeps the board pair-interleaved in HBM."""
-    return device_ilv(width, topology) == 2
-
-
 def device_layout(width: int, topology: int = GOL_TORUS) -> int:
     """libgol's own answer (gol_device_layout) -- device_ilv restates it."""
     k = ctypes.c_int32(0)

@@ -38,6 +38,14 @@ def test_all_coordinates_inclusive():
     assert B.board_cells((6, 6)) == (7, 7)
 
 
+def test_iter_positions_follows_generate_all_coordinates():
+    # the CellStateMsg payload order: x-major, (x, y) with cells[y, x]
+    cells = (np.random.default_rng(3).random((7, 7)) < 0.5).astype(np.uint8)
+    got = list(B.iter_positions(cells))
+    assert [p for p, _ in got] == B.generate_all_coordinates((6, 6))
+    assert all(s == bool(cells[y, x]) for (x, y), s in got)
+
+
 def test_logger_format():
     cells = np.array([[1, 0, 1], [0, 1, 0], [0, 0, 0]], dtype=np.uint8)
     lines = B.LoggerActor.format_epoch(cells, 4)
