@@ -275,6 +275,9 @@ int main(int argc, char** argv) {
     };
     bool quiet = false;
     try {
+        if (gol_abi_version() != GOL_ABI_VERSION)
+            throw std::runtime_error("libgol ABI version " + std::to_string(gol_abi_version()) +
+                                     ", this frontend was built against " + std::to_string(GOL_ABI_VERSION));
         for (int i = 1; i < argc; ++i) {
             std::string a = argv[i];
             if (a == "--quiet") { quiet = true; continue; }

@@ -26,6 +26,9 @@ GOL_ENODEV = 6
 GOL_TORUS = 0
 GOL_REF_CLIPPED = 1
 GOL_UNIQUE_ID_BYTES = 128
+# include/gol.h GOL_ABI_VERSION this binding is written against (2: the
+# canonical state hash)
+GOL_ABI_VERSION = 2
 
 
 class GolError(RuntimeError):
@@ -155,6 +158,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.gol_abi_version() != GOL_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI version {lib.gol_abi_version()}, this binding needs "
+                          f"{GOL_ABI_VERSION}; rebuild it")
     return lib
 
 
