@@ -54,6 +54,39 @@ def test_checkpoint_roundtrip_and_reshard(tmp_path):
     assert (E.parse_checkpoint(E.assemble_checkpoint(str(tmp_path), 40, 3, 20))[1] == board[3:23]).all()
 
 
+def test_checkpoint_rows_reads_any_row_list(tmp_path):
+    """checkpoint_rows seeks to runs of consecutive rows: any row list --
+    unsorted, repeated, wrapping, across files of two decompositions -- comes
+    back as those rows of the board; rows no file holds, and a file whose
+    header disagrees with its name, are refused."""
+    W, H = 32 * 3, 41
+    board = O.seed_packed(W, H, 11)
+    rng = np.random.default_rng(7)
+    for epoch in range(6):
+        d = str(tmp_path / f"c{epoch}")
+        cuts = sorted(set(rng.integers(1, H, size=int(rng.integers(0, 6))).tolist()))
+        for r0, r1 in zip([0] + cuts, cuts + [H]):
+            E.write_shard_checkpoint(d, _blob(W, H, r0, r1 - r0, epoch, board))
+        if epoch % 2:  # a merged block overlapping the others
+            E.write_shard_checkpoint(d, _blob(W, H, 5, 20, epoch, board))
+        for _ in range(8):
+            idx = rng.integers(0, H, size=int(rng.integers(1, 3 * H))).tolist()
+            if rng.random() < 0.5:
+                a = int(rng.integers(0, H))
+                idx = [(a + k) % H for k in range(int(rng.integers(1, H)))]  # a wrapping run
+            assert (E.checkpoint_rows(d, epoch, idx) == board[idx]).all()
+    d = str(tmp_path / "gap")
+    E.write_shard_checkpoint(d, _blob(W, H, 0, 10, 0, board))
+    E.write_shard_checkpoint(d, _blob(W, H, 12, 29, 0, board))
+    assert (E.checkpoint_rows(d, 0, [9, 12]) == board[[9, 12]]).all()
+    with pytest.raises(FileNotFoundError):
+        E.checkpoint_rows(d, 0, [9, 10])
+    os.replace(os.path.join(E.epoch_dir(d, 0), "r0000000000_10.gol"),
+               os.path.join(E.epoch_dir(d, 0), "r0000000010_10.gol"))
+    with pytest.raises(ValueError):
+        E.checkpoint_rows(d, 0, [11])
+
+
 def test_light_cone_rows(tmp_path):
     W, H = 32 * 3, 20
     board = O.seed_packed(W, H, 8)
