@@ -745,12 +745,20 @@ def ring_fault_drill(eng, make_engine, join, rank: int, world: int, width: int, 
         epoch += n
         # a checkpoint every `every` generations; the lost rank dies right
         # after its last step, before it could write one
-        if epoch % every == 0 and not (rank == victim and epoch == kill_at):
+        if epoch % every == 0:
             t = time.perf_counter()
-            path = write_shard_checkpoint(ckpt_dir, eng.checkpoint())
-            if my_file and my_file != path:
-                os.unlink(my_file)  # every rank passed this epoch's checkpoint before the next step
-            my_file, ckpt_s = path, ckpt_s + time.perf_counter() - t
+            wrote = not (rank == victim and epoch == kill_at)
+            path = write_shard_checkpoint(ckpt_dir, eng.checkpoint()) if wrote else None
+            # An epoch's checkpoint is complete once every rank has written
+            # its file; only then may a rank drop its previous one.  A rank
+            # lost at a checkpoint epoch (kill_at % every == 0) leaves that
+            # epoch incomplete, so the previous files stay for its recovery.
+            complete = int(eng.allreduce_u64(np.array([int(wrote)], dtype=np.uint64))[0]) == world
+            if complete and my_file and my_file != path:
+                os.unlink(my_file)
+            if wrote and (complete or my_file is None):
+                my_file = path
+            ckpt_s += time.perf_counter() - t
     rep["before"] = before
     rep["checkpoint_s"] = round(ckpt_s, 3)
     rep["run_to_loss_s"] = round(time.perf_counter() - t_run, 3)
