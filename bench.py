@@ -36,6 +36,12 @@ HBM -- temporal blocking fuses 6-8 generations per pass over the plane.  So:
     clock, frac = achieved / peak; roofline.held_clock prices the same launches
     at the clock they actually held (in-kernel probe, gol_profile_clock) as an
     issue-efficiency diagnostic, with the PMC clock (profiles/) beside it;
+  * roofline.frac_guide_issue prices the same launches at the guide's 2 cycles
+    per wave64 VALU instruction (MI355X_MICROARCH.md) instead of the measured
+    per-op costs, and roofline.issue_rate gives the wave-VALU instructions per
+    cycle per SIMD the launches issued (0.5 = that ceiling);
+  * roofline.copy_peak = the measured stream-copy peak (profiles/copy_peak.json,
+    scripts/micro/copy_bw.hip); single-generation lines add frac_of_copy_peak;
   * roofline.traffic = PMC HBM bytes per launch, and roofline.hbm the physical
     HBM bandwidth that implies against the 8 TB/s spec;
   * roofline.hbm_effective = SURVEY.md section 8(d)'s 2 bits per cell-update,
@@ -74,6 +80,12 @@ VALU_MIX = {"v_bitop3_b32": (7, 2.3), "v_xor_b32": (0.5, 2.3), "v_and_b32": (0.5
             "v_alignbit_b32": (1, 4.1), "v_mov_b32_dpp": (1, 4.3)}
 # The fused hash adds one v_mad_u64_u32 per word and generation (DESIGN.md "State hash").
 VALU_MIX_HASH = dict(VALU_MIX, v_mad_u64_u32=(1, 4.6))
+# MI355X_MICROARCH.md (CU / SIMD model): a wave64 VALU instruction issues over
+# 2 cycles on its SIMD -- the guide's rate, which prices frac_guide_issue
+# whatever the instructions are (the mix-priced frac uses the measured per-op
+# costs above instead).
+GUIDE_CYCLES_PER_VALU = 2.0
+COPY_PEAK_FILE = os.path.join("profiles", "copy_peak.json")
 
 
 def parse():
@@ -164,7 +176,10 @@ class Job:
                 except OSError:
                     pass
                 if time.monotonic() - t0 > timeout:
-                    raise SystemExit(f"rank {rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s")
+                    raise SystemExit(f"rank {rank}: no RCCL id from rank 0 at {path} after {timeout:.0f} s (the file "
+                                     "is keyed by MASTER_ADDR:MASTER_PORT and the launch: GOL_BENCH_RUN_ID if set, "
+                                     "else the ranks' common parent process -- a launcher whose ranks have "
+                                     "different parents must set GOL_BENCH_RUN_ID to one value on every rank)")
                 time.sleep(0.01)
         eng.comm_init(uid, rank, world)
         if world > 1:
@@ -338,13 +353,56 @@ def _cpu_rate(O, width, H, threads, seconds):
     return width * H * gens / dt / 1e9, gens, dt
 
 
+SCALAR_EDGE = 4096
+# The reference's own ceiling: its default board is
+# size (6, 6), i.e. the inclusive 7 x 7 = 49 cells (application.conf:31-33,
+# BoardCreator.scala:47-53), and the frontend advances at most one generation
+# per `tick` = 3000 ms (application.conf:40, BoardCreator.scala:105-116).
+AKKA_CELLS, AKKA_TICK_S = 49, 3.0
+
+
+def _scalar_rate(O, seconds):
+    """The scalar per-cell oracle (oracle_step_cells, gol_oracle.c: the literal
+    restatement of package.scala:17-28 + NextStateCellGathererActor.scala:39-46,
+    one thread) on the 4096^2 torus from the golden seed, for at least one
+    generation and about `seconds`; the board it ends on is checked against
+    tests/golden/golden.json's per-generation hashes."""
+    E = SCALAR_EDGE
+    cells = O.unpack(O.seed_packed(E, E, GOLDEN_SEED), E)
+    gens, t0 = 0, time.perf_counter()
+    while gens == 0 or time.perf_counter() - t0 < seconds:
+        cells = O.step_cells(cells, O.TORUS, O.LIFE)
+        gens += 1
+    dt = time.perf_counter() - t0
+    h = O.hash_packed(O.pack(cells), E)
+    golden = None
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            for ent in json.load(f)["torus"]:
+                if (ent["W"], ent["H"], ent["seed"], ent["rule"]) == (E, E, GOLDEN_SEED, "life") and gens <= ent["gens"]:
+                    golden = int(ent["hashes"][gens - 1])
+    except (OSError, ValueError, KeyError):
+        pass
+    return E * E * gens / dt / 1e9, gens, dt, {"epoch": gens, "hash": f"{h:#018x}",
+                                              "golden": None if golden is None else f"{golden:#018x}",
+                                              "match": None if golden is None else h == golden}
+
+
 def cpu_baseline(width, seconds):
-    """Oracle (bit-packed, bit-sliced, OpenMP) on a bounded sample of the same
-    workload: a torus of the same width and 1024 rows, run for ~`seconds`,
-    on the CPU share the harness grants the job (OMP_NUM_THREADS: 16 threads
-    per GPU on the pool's boxes; sched_getaffinity when unset).  More threads
-    than the job's cgroup quota would only time-slice on the same CPUs, so no
-    such figure is reported."""
+    """The CPU figures of SURVEY.md section 8(d), each on a bounded sample:
+
+    * packed_port (the line's value): the oracle's bit-packed, bit-sliced,
+      OpenMP step on a torus of the same width and 1024 rows, run for
+      ~`seconds`, on the CPU share the harness grants the job
+      (OMP_NUM_THREADS: 16 threads per GPU on the pool's boxes;
+      sched_getaffinity when unset).  More threads than the job's cgroup
+      quota would only time-slice on the same CPUs, so no such figure is
+      reported;
+    * scalar_4096: the scalar per-cell oracle, one thread, on configs[1]'s
+      4096^2 torus (about `seconds`), its end state checked against the
+      golden hashes;
+    * akka_derived_ceiling: the reference's own rate bound, derived (not
+      measured: no JVM on the box) from its default board and tick."""
     from oracle import oracle as O
     affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
@@ -361,6 +419,21 @@ def cpu_baseline(width, seconds):
                      f"slice of the same workload, {gens} generations in {dt:.1f} s on {threads} threads"}
     if quota:
         out["cgroup_cpu_quota"] = quota
+    out["packed_port"] = {k: out[k] for k in ("value", "unit", "cores", "kind", "sample")}
+    out["packed_port"]["model"] = "bit-packed 32 cells per word, bit-sliced adder, OpenMP over rows"
+    vs, gs, dts, par = _scalar_rate(O, seconds)
+    out["scalar_4096"] = {"value": round(vs, 5), "unit": "GCUPS", "cores": 1, "kind": "port",
+                          "model": "scalar per-cell oracle (oracle_step_cells): 8 wrapped neighbour reads and a "
+                                   "rule lookup per cell, the reference's per-cell algorithm restated",
+                          "sample": f"{SCALAR_EDGE}x{SCALAR_EDGE} torus B3/S23 (BASELINE.json configs[1]) from seed "
+                                    f"0x5EED, {gs} generations in {dts:.1f} s on 1 thread",
+                          "parity": par}
+    out["akka_derived_ceiling"] = {
+        "value": AKKA_CELLS / AKKA_TICK_S / 1e9, "unit": "GCUPS", "cores": None, "kind": "derived",
+        "cell_updates_per_s": round(AKKA_CELLS / AKKA_TICK_S, 3),
+        "sample": "not measured (no JVM on the box): the reference's default 7 x 7 board (size (6, 6), "
+                  "application.conf:31-33) advances at most one generation per 3000 ms tick "
+                  "(application.conf:40, BoardCreator.scala:105-116) = 49 / 3 cell updates per second"}
     return out
 
 
@@ -413,6 +486,33 @@ def valu_peak_gcups(mix, clock_ghz):
     return SIMDS * clock_ghz * 1e9 / cycles * CELLS_PER_WAVE_INSTR / 1e9, cycles
 
 
+def guide_peak_gcups(valu_per_word_gen, clock_ghz=CLOCK_MAX_GHZ):
+    """VALU-issue ceiling at the guide's 2 cycles per wave64 instruction:
+    every SIMD issuing one instruction per 2 cycles at `clock_ghz`, each
+    instruction one word (32 cells) on each of 64 lanes."""
+    return SIMDS * clock_ghz * 1e9 / (valu_per_word_gen * GUIDE_CYCLES_PER_VALU) * CELLS_PER_WAVE_INSTR / 1e9
+
+
+def issue_rate(gcups, valu_per_word_gen, clock_ghz):
+    """Wave-VALU instructions issued per cycle per SIMD by launches running
+    at `gcups` with `valu_per_word_gen` instructions per word-generation at
+    `clock_ghz` (0.5 = the guide's issue ceiling)."""
+    return gcups * 1e9 / CELLS_PER_WAVE_INSTR * valu_per_word_gen / (SIMDS * clock_ghz * 1e9)
+
+
+def copy_peak():
+    """The measured stream-copy peak (read + write GB/s): profiles/copy_peak.json,
+    written from scripts/micro/copy_bw.hip's last line on an MI355X box.
+    None if absent."""
+    try:
+        with open(os.path.join(ROOT, COPY_PEAK_FILE)) as f:
+            d = json.load(f)
+        return {"gbs": float(d["copy_peak_gbs"]), "variant": d.get("variant"),
+                "source": f"{COPY_PEAK_FILE} ({d.get('measured', 'scripts/micro/copy_bw.hip')})"}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def compact_plan(plan):
     """A long pass plan as "n x G" runs, e.g. "128 x 8" or "7 x 12 + 2 x 9"."""
     runs = []
@@ -441,6 +541,10 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
         r = {"bound": "hbm", "achieved": round(algo / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
              "frac": round(algo / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
              "algorithmic_bytes_per_launch": algo, **common}
+        cp = copy_peak()
+        if cp:
+            r["copy_peak"] = cp
+            r["frac_of_copy_peak"] = round(algo / avg_s / 1e9 / cp["gbs"], 4)
         if pmc:
             r["traffic"] = round(pmc["hbm_bytes"])
             r["measured_hbm_gbs"] = round(pmc["hbm_bytes"] / avg_s / 1e9, 1)
@@ -454,8 +558,16 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
     # these launches actually held (in-kernel probe, gol_profile_clock) only
     # prices the separate issue-efficiency diagnostic under held_clock.
     peak_max, cycles = valu_peak_gcups(mix, CLOCK_MAX_GHZ)
+    n_valu = sum(n for n, _ in mix.values())
+    peak_guide = guide_peak_gcups(n_valu)
     r = {"bound": "valu", "achieved": round(gcups, 1), "peak": round(peak_max, 1), "unit": "GCUPS",
-         "frac": round(gcups / peak_max, 4), "traffic": round(pmc["hbm_bytes"]) if pmc else None,
+         "frac": round(gcups / peak_max, 4), "frac_kind": "mix-priced: the loop's instruction mix at the measured "
+                                                          "per-op issue costs (profiles/r01_valu_op_costs.txt)",
+         "frac_guide_issue": round(gcups / peak_guide, 4),
+         "peak_guide_issue": round(peak_guide, 1),
+         "guide_issue_note": f"{n_valu:g} VALU per word-generation at the guide's {GUIDE_CYCLES_PER_VALU:g} cycles "
+                             "per wave64 instruction (MI355X_MICROARCH.md), 2.4 GHz",
+         "traffic": round(pmc["hbm_bytes"]) if pmc else None,
          "traffic_source": ("profiles/pmc_launch.json " + ", ".join(pmc["keys"]) +
                             " (rocprofv3 PMC passes of the same kernels; not measured in this run)") if pmc else None,
          "peak_clock_ghz": CLOCK_MAX_GHZ,
@@ -466,6 +578,17 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
                   "source": "loop census scripts/isa_loop.py; issue costs profiles/r01_valu_op_costs.txt"},
          **common}
     held = {"clock_pmc_ghz": round(pmc["clock_ghz"], 3) if pmc else None}
+    vpwg = pmc["valu_per_word_gen"] if pmc else n_valu
+    clk_issue = clock or (pmc["clock_ghz"] if pmc else None)
+    if clk_issue:
+        r["issue_rate"] = {"wave_valu_per_cycle_per_simd": round(issue_rate(gcups, vpwg, clk_issue), 4),
+                           "guide_max": round(1 / GUIDE_CYCLES_PER_VALU, 4), "clock_ghz": round(clk_issue, 3),
+                           "valu_per_word_generation": round(vpwg, 3),
+                           "source": ("PMC VALU per word-generation" if pmc else "loop census") + " at the " +
+                                     ("in-kernel probe clock" if clock else "PMC clock")}
+    cp = copy_peak()
+    if cp:
+        r["copy_peak"] = cp
     if clock:
         peak_held, _ = valu_peak_gcups(mix, clock)
         held.update({"ghz": round(clock, 3), "peak_at_held_clock": round(peak_held, 1),
@@ -917,15 +1040,24 @@ def main():
         # lost rank -- a path that has not met every multi-GPU fabric yet.  A
         # watchdog keeps it from costing the line: past --fault-timeout every
         # rank stops, rank 0 printing the line with the drill marked timed out.
+        import copy
         import threading
+
+        # What the watchdog prints is fixed before the drill starts: the
+        # drill keeps appending to parity.checks on the main thread, which
+        # the timer thread must not read mid-update.
+        line_before = copy.deepcopy(dict(out, parity=parity.report()))
+        failed_before = parity.failed(a.allow_unchecked)
 
         def give_up():
             msg = f"fault drill did not finish within {a.fault_timeout:.0f} s"
             if rank == 0:
-                out["fault_recovery"] = {"status": "timed out", "timeout_s": a.fault_timeout}
-                out["parity_failed"] = parity.failed(a.allow_unchecked) + [msg]
-                out["parity_ok"] = False
-                os.write(result_fd, (json.dumps(out) + "\n").encode())
+                line = dict(line_before, fault_recovery={"status": "timed out", "timeout_s": a.fault_timeout,
+                                                          "note": "a rank that raised inside the drill reports "
+                                                                  "its exception on its own stderr"})
+                line["parity_failed"] = failed_before + [msg]
+                line["parity_ok"] = False
+                os.write(result_fd, (json.dumps(line) + "\n").encode())
             print(f"bench.py rank {rank}: {msg}", file=sys.stderr, flush=True)
             os._exit(4)
 

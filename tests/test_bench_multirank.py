@@ -241,7 +241,10 @@ def test_fault_drill_watchdog(tmp_path):
                    "--fault-timeout", "8", extra_env={"FAKE_HANG_REJOIN": "1"}, rc=None)
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert d["value"] > 0 and d["parity"]["match"] is True  # the measured windows are intact
-    assert d["fault_recovery"] == {"status": "timed out", "timeout_s": 8.0}
+    fr = d["fault_recovery"]
+    assert (fr["status"], fr["timeout_s"]) == ("timed out", 8.0) and "stderr" in fr["note"]
+    # the line is the snapshot taken before the drill: none of its checks leaked in
+    assert not any("fault drill" in c["what"] for c in d["parity"]["checks"])
     assert d["parity_ok"] is False and any("fault drill" in f for f in d["parity_failed"])
 
 

@@ -83,3 +83,57 @@ def test_probe_clock_prices_only_the_issue_efficiency(monkeypatch):
     assert abs(r["peak"] - round(peak_max, 1)) < 0.2
     assert abs(hc["issue_efficiency"] * peak_held - r["frac"] * peak_max) < 5
     assert r["frac"] < hc["issue_efficiency"] and r["traffic"] == 18e9
+
+
+def test_guide_issue_fraction_and_issue_rate(monkeypatch):
+    """frac_guide_issue prices the launches at the guide's 2 cycles per wave64
+    VALU instruction (10 instructions per word-generation: 20 cycles); the
+    issue rate is wave-VALU per cycle per SIMD at the held clock (<= 0.5)."""
+    ent = {"launch_ms": 5.4, "hbm_bytes": 17.6e9, "clock_ghz": 2.0, "valu_per_word_gen": 10.2,
+           "generations_per_launch": 10}
+    _table(monkeypatch, {"262144x262144/N1/G10/h0": ent})
+    cells = 262144 * 262144
+    r = bench.roofline(kms=10.84, launches=2, gens_covered=20, cells=cells, plan=[10, 10],
+                       shape="262144x262144", mode="N1", clock=2.01)
+    guide = 1024 * 2.4e9 / 20 * 2048 / 1e9
+    assert abs(r["peak_guide_issue"] - guide) < 0.2
+    assert abs(r["frac_guide_issue"] - r["achieved"] / guide) < 1e-3 and r["frac_guide_issue"] < r["frac"]
+    ir = r["issue_rate"]
+    want = r["achieved"] * 1e9 / 2048 * 10.2 / (1024 * 2.01e9)
+    assert abs(ir["wave_valu_per_cycle_per_simd"] - want) < 1e-3 and ir["guide_max"] == 0.5
+    assert ir["clock_ghz"] == 2.01 and ir["valu_per_word_generation"] == 10.2
+    assert "mix-priced" in r["frac_kind"]
+
+
+def test_issue_rate_uses_the_pmc_clock_without_a_probe(monkeypatch):
+    ent = {"launch_ms": 5.4, "hbm_bytes": 17.6e9, "clock_ghz": 2.0, "valu_per_word_gen": 10.0,
+           "generations_per_launch": 10}
+    _table(monkeypatch, {"262144x262144/N1/G10/h0": ent})
+    r = bench.roofline(kms=10.84, launches=2, gens_covered=20, cells=262144 * 262144, plan=[10, 10],
+                       shape="262144x262144", mode="N1")
+    assert r["issue_rate"]["clock_ghz"] == 2.0 and "PMC clock" in r["issue_rate"]["source"]
+    _table(monkeypatch, {})
+    r = bench.roofline(kms=10.84, launches=2, gens_covered=20, cells=262144 * 262144, plan=[10, 10],
+                       shape="262144x262144", mode="N1")
+    assert "issue_rate" not in r  # no clock at all: no rate
+
+
+def test_copy_peak_and_single_generation_fraction(monkeypatch):
+    monkeypatch.setattr(bench, "copy_peak", lambda: {"gbs": 6000.0, "variant": "x", "source": "profiles/copy_peak.json"})
+    _table(monkeypatch, {})
+    r = bench.roofline(kms=20.4, launches=102, gens_covered=102, cells=65536 * 65536, plan=[1] * 102,
+                       shape="65536x65536", mode="N1")
+    assert r["copy_peak"]["gbs"] == 6000.0
+    assert abs(r["frac_of_copy_peak"] - r["achieved"] / 6000.0) < 1e-3
+    r = bench.roofline(kms=10.84, launches=2, gens_covered=20, cells=262144 * 262144, plan=[10, 10],
+                       shape="262144x262144", mode="N1")
+    assert r["copy_peak"]["source"].startswith("profiles/") and "frac_of_copy_peak" not in r
+
+
+def test_committed_copy_peak_file():
+    """profiles/copy_peak.json, when present, carries the measured rate and
+    where it came from."""
+    cp = bench.copy_peak()
+    if cp is None:
+        return
+    assert 3000 < cp["gbs"] < bench.HBM_PEAK_GBS and cp["source"].startswith("profiles/copy_peak.json")
