@@ -17,11 +17,16 @@
 //   game-of-life.simulation.shards            shards (default = gpus); > 1 runs an in-process group
 //   game-of-life.log.file                     LoggerActor output (default info.log, "-" = stdout)
 //   game-of-life.log.every                    log the board every N epochs (0 = never; default 1)
+//   game-of-life.log.full                     false (default): the reference's dump shape; true: the
+//                                             whole board (this build's extension)
 //
 // Output: "Epoch: N" per tick on stdout (BoardCreator.scala:115) unless
 // --quiet, "hash N 0x<16 hex>" per generation, and the LoggerActor board
-// dump ("At epoch:N", dashes, rows "[a,b,...]", LoggerActor.scala:36-44) --
-// positional here (the reference prints cells in arrival order).
+// dump in the reference's shape for board size (x, y): "At epoch:N", 2x+1
+// dashes, y rows "[a,b,...]" of x entries, the dashes again and an empty line
+// (LoggerActor.scala:17,28,36-44) -- the cells of columns 0..x-1 and rows
+// 0..y-1, positional here (the reference prints x*y of the (x+1)*(y+1) cells
+// in arrival order).  log.full=true prints every row and column instead.
 #include <chrono>
 #include <cinttypes>
 #include <cstdio>
@@ -123,7 +128,7 @@ std::vector<uint8_t> java_random_board(int w, int h, int64_t seed) {
     return cells;
 }
 
-// LoggerActor.scala:17-19,36-44 text format.
+// LoggerActor.scala:17-19,36-44 text format: `x` entries per row, `y` rows.
 class LoggerActor {
   public:
     LoggerActor(int x, int y, const std::string& path) : x_(x), y_(y) {
@@ -226,8 +231,10 @@ class BoardCreator {
 
     int64_t tick_ms() const { return tick_ms_; }
     int64_t words_per_row() const { return (width_ + 31) / 32; }
-    int x() const { return torus_ ? x_ : x_ + 1; }
-    int y() const { return torus_ ? y_ : y_ + 1; }
+    int x() const { return torus_ ? x_ : x_ + 1; }  // cells per row
+    int y() const { return torus_ ? y_ : y_ + 1; }  // rows
+    int size_x() const { return x_; }               // board size (x, y) (application.conf:31-33)
+    int size_y() const { return y_; }
     uint64_t step() const { return step_; }
 
   private:
@@ -272,6 +279,7 @@ int main(int argc, char** argv) {
         {"game-of-life.simulation.gpus", "1"},
         {"game-of-life.log.file", "info.log"},
         {"game-of-life.log.every", "1"},
+        {"game-of-life.log.full", "false"},
     };
     bool quiet = false;
     try {
@@ -298,7 +306,11 @@ int main(int argc, char** argv) {
         if (!cfg.count("game-of-life.simulation.shards"))
             cfg["game-of-life.simulation.shards"] = cfg["game-of-life.simulation.gpus"];
         BoardCreator board(cfg);
-        LoggerActor logger(board.x(), board.y(), cfg["game-of-life.log.file"]);
+        // the reference's LoggerActor(boardSize): x*y cells per epoch
+        // (LoggerActor.scala:28); log.full: the whole board
+        const bool full = cfg["game-of-life.log.full"] == "true";
+        LoggerActor logger(full ? board.x() : board.size_x(), full ? board.y() : board.size_y(),
+                           cfg["game-of-life.log.file"]);
         const int64_t gens = std::stoll(cfg["game-of-life.simulation.generations"]);
         const int64_t every = std::stoll(cfg["game-of-life.log.every"]);
         board.start_simulation();

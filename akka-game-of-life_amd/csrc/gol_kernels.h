@@ -1,5 +1,6 @@
 // gol_kernels.h -- internal interface between the C-ABI host layer
-// (gol_capi.cpp) and the gfx950 kernels (gol_kernels.hip).  Not installed.
+// (gol_capi.cpp and the units gol_ctx.h lists) and the gfx950 kernels
+// (gol_stencil.h, gol_step_g<G>.hip, gol_misc.hip).  Not installed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -1113,8 +1113,8 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
 // lanes it needs 183-270 registers or spills (1-1.6 KB scratch per lane), so
 // VEC = 4 (gol_set_tuning's words_per_lane = 4) runs the vertical-first
 // kernel.  Its generic-rule and clipped instances deeper than
-// kMaxGensVec4Generic spill and are neither built nor launched (gol_capi.cpp
-// refuses such a tuning).
+// kMaxGensVec4Generic spill and are neither built nor launched (gol_set_tuning
+// in gol_capi.cpp refuses such a tuning).
 template <int VEC, int G, bool LIFE, bool CLIPPED>
 constexpr bool kBuilt = G == 1 || VEC <= 2 || (LIFE && !CLIPPED) || G <= kMaxGensVec4Generic;
 

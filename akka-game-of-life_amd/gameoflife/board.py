@@ -60,30 +60,41 @@ class SimulationParams:
 class LoggerActor:
     """LoggerActor.scala:30-46 output format.
 
-    The reference prints, per epoch, ``At epoch:N``, a dash line of length
-    2x+1, rows ``[a,b,...]`` and a closing dash line.  It fills the rows
-    from CellStateMsgs in *arrival order* (:32-33 prepend, :17 slice) and
-    prints once x*y of the (x+1)*(y+1) messages have arrived (:28,35), so
-    its rows are neither positional nor complete.  This port keeps the
-    format but prints the whole board positionally: one row per board row,
-    one entry per cell (the native frontend, csrc/gol_frontend.cpp, prints
-    the same text).
+    For a board of size (x, y) the reference prints, per epoch, ``At
+    epoch:N``, a dash line of length 2x+1 (:42), y rows (:40) of x entries
+    each (:17 slices x messages per row) as ``[a,b,...]`` (:19) and a
+    closing dash line followed by an empty line (:44).  It prints once x*y
+    CellStateMsgs of the epoch have arrived (:28,35) -- of the (x+1)*(y+1)
+    cells the board holds (BoardCreator.scala:47-53) -- filling the rows in
+    arrival order (:32-33 prepend).  The arrival order cannot be reproduced;
+    the shape can: this logger prints the x*y cells of columns 0..x-1 and
+    rows 0..y-1, positionally.  ``full=True`` is this build's extension:
+    every row and column of the board (same format, dash line 2w+1 for a
+    board w cells wide).  The native frontend (csrc/gol_frontend.cpp) prints
+    the same text (``log.full``).
     """
 
-    def __init__(self, board_size: BoardSize, sink: Callable[[str], None] | None = None):
+    def __init__(self, board_size: BoardSize, sink: Callable[[str], None] | None = None, full: bool = False):
         self.board_size = board_size
+        self.full = full
         self.lines: list[str] = []
         self.sink = sink or self.lines.append
 
     @staticmethod
-    def format_epoch(cells: np.ndarray, epoch: int) -> list[str]:
+    def format_epoch(cells: np.ndarray, epoch: int, size: BoardSize | None = None) -> list[str]:
+        """The epoch's text.  size = (x, y): the reference's shape, y rows of
+        x entries (cells[:y, :x]); None: all of `cells` (the full-board
+        extension)."""
+        if size is not None:
+            x, y = size
+            cells = cells[:y, :x]
         h, w = cells.shape
         rows = ["[" + ",".join(str(int(v)) for v in cells[r]) + "]" for r in range(h)]
         dash = "-" * (w * 2 + 1)
         return [f"At epoch:{epoch}", dash, *rows, dash + "\n"]
 
     def log_board(self, cells: np.ndarray, epoch: int) -> None:
-        for line in self.format_epoch(cells, epoch):
+        for line in self.format_epoch(cells, epoch, None if self.full else self.board_size):
             self.sink(line)
 
 

@@ -55,7 +55,7 @@ import numpy as np
 
 from .shard import shard_rows_py
 
-# CkptHeader of gol_capi.cpp: magic[8], width, height, row0, rows, wwords,
+# CkptHeader of gol_ctx.h: magic[8], width, height, row0, rows, wwords,
 # epoch, topology, birth, survive, pad
 _HDR = struct.Struct("<8s5qQiIIi")
 _MAGIC = b"GOLCKPT1"

@@ -5,7 +5,7 @@ random node (BoardCreator.scala:33-36,65-70); neighbours then talk across the
 network (application.conf:11-17).  Here rank r of n owns the contiguous row
 block ``gol_shard_rows(H, r, n)``.  Before every pass of G generations it
 exchanges G halo rows with each ring neighbour over RCCL (inside libgol,
-gol_capi.cpp one_pass): its first G rows go up, its last G rows go down, and
+gol_ring.cpp one_pass): its first G rows go up, its last G rows go down, and
 G-row halos come back.  This module holds the host-side pieces: the halo plan
 (the exact op order and message shapes libgol issues, shared with the CPU
 tests), the pass-depth cap, the hash reduction and the per-process backend
@@ -28,11 +28,11 @@ def shard_rows_py(height: int, rank: int, nranks: int) -> tuple[int, int]:
 
 
 MAX_GENS_PER_PASS = 12  # gol_kernels.h kMaxGensPerPass
-MAX_GENS_PLANNED_GENERIC = 8  # gol_capi.cpp kMaxGensPlannedGeneric
+MAX_GENS_PLANNED_GENERIC = 8  # gol_schedule.cpp kMaxGensPlannedGeneric
 
 
 def ring_depth_cap(height: int, nranks: int, gens_per_pass: int = 0, life_torus: bool = True) -> int:
-    """Deepest pass a ring may run (gol_capi.cpp depth_cap): every rank must
+    """Deepest pass a ring may run (gol_schedule.cpp depth_cap): every rank must
     issue identical halo messages, so the depth is capped by the smallest
     shard, floor(H / N) rows (a 1-rank self-ring: H).  Planned passes of
     other rules / the clipped topology stop at 8."""
@@ -41,7 +41,7 @@ def ring_depth_cap(height: int, nranks: int, gens_per_pass: int = 0, life_torus:
 
 
 def fixed_depth_plan(generations: int, depth: int) -> list[int]:
-    """Pass depths of a fixed gens_per_pass (gol_capi.cpp plan_passes: taken
+    """Pass depths of a fixed gens_per_pass (gol_schedule.cpp plan_passes: taken
     literally, the last pass shorter)."""
     plan, done = [], 0
     while done < generations:
@@ -52,7 +52,7 @@ def fixed_depth_plan(generations: int, depth: int) -> list[int]:
 
 @dataclasses.dataclass(frozen=True)
 class HaloPlan:
-    """Halo exchange of one rank before each pass (gol_capi.cpp one_pass).
+    """Halo exchange of one rank before each pass (gol_ring.cpp one_pass).
 
     A pass of G generations sends the rank's last G rows down and its first G
     rows up, and receives the G rows above it (top halo) and below it (bottom

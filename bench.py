@@ -718,7 +718,7 @@ def ring_stats(st, passes):
 
 def ring_schedule_runs(GolEngine, N, a, local, eng, W, H, parity):
     """N = 1 only: the row-sharded (RCCL ring) schedule on this GPU, as a 1-rank
-    self-ring (gol_capi.cpp one_pass: interior launch || G-row halo
+    self-ring (gol_ring.cpp one_pass: interior launch || G-row halo
     ncclSend/ncclRecv to itself, then the boundary rows on the edge stream).
     (1) the whole board, (2) one rank's shard of the N = 8 decomposition
     (262144 x 32768): what each of 8 ranks computes, without the xGMI latency

@@ -3,7 +3,7 @@
 (reseed, the 5-generation warm-up at the automatic plan, then the timed
 passes, each at a fixed depth and band), interleaved rounds, in one process.
 Run it with GOL_TAIL=1.0,3 so fixed bands keep the default tail split of wide
-boards (gol_capi.cpp tail_split).
+boards (gol_schedule.cpp tail_split).
 
     GOL_TAIL=1.0,3 python scripts/band_ab.py [--shape WxH] [--rounds R] 12:384,8:256 12:768,8:512 ...
 

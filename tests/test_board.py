@@ -52,6 +52,25 @@ def test_logger_format():
     assert lines == ["At epoch:4", "-------", "[1,0,1]", "[0,1,0]", "[0,0,0]", "-------\n"]
 
 
+def test_logger_reference_shape_at_default_board():
+    """Board size (6, 6): the reference prints 2x+1 = 13 dashes and y = 6
+    rows of x = 6 entries (LoggerActor.scala:17,28,36-44), of the 7 x 7 cells
+    the board holds; full=True prints all 7 x 7 (this build's extension)."""
+    cells = O.java_random_cells(6, 6, 42)
+    out = []
+    B.LoggerActor((6, 6), sink=out.append).log_board(cells, 3)
+    assert out[0] == "At epoch:3" and out[1] == "-" * 13 and out[-1] == "-" * 13 + "\n"
+    rows = out[2:-1]
+    assert len(rows) == 6 and all(len(r[1:-1].split(",")) == 6 for r in rows)
+    assert rows == ["[" + ",".join(str(int(v)) for v in cells[y, :6]) + "]" for y in range(6)]
+    full = []
+    B.LoggerActor((6, 6), sink=full.append, full=True).log_board(cells, 3)
+    assert full[1] == "-" * 15 and len(full) == 7 + 3 and full[2:-1][:6] != rows
+    # non-square size (x, y) = (4, 2): 2 rows of 4
+    lines = B.LoggerActor.format_epoch(O.java_random_cells(4, 2, 1), 1, size=(4, 2))
+    assert lines[1] == "-" * 9 and len(lines) == 2 + 3 and all(len(r.split(",")) == 4 for r in lines[2:-1])
+
+
 def test_config_keys_and_durations():
     text = """
     // same shape as the reference's application.conf game-of-life section
@@ -122,8 +141,8 @@ def test_board_creator_drives_backend_and_logs():
     bc.next_step(3)
     assert bc.step == 5
     # logged after ticks reaching epochs 1, 2 and 5 (one multi-generation tick)
-    assert logger.lines[0] == "At epoch:1" and len(logger.lines) == 3 * (7 + 3)
-    assert logger.lines[20] == "At epoch:5"
+    assert logger.lines[0] == "At epoch:1" and len(logger.lines) == 3 * (6 + 3)
+    assert logger.lines[18] == "At epoch:5" and logger.lines[1] == "-" * 13
     assert bc.send_me_my_neighbours((0, 0)) == [(0, 1), (1, 0), (1, 1)]
 
 

@@ -38,8 +38,10 @@ def test_frontend_reference_board_golden(gpu, tmp_path, shards):
             assert hashes == res["hashes"], (entry["java_seed"], name, shards)
             final = np.array([[int(ch) for ch in row] for row in res["boards"][-1]["cells"]],
                              dtype=np.uint8)
-            want = "\n".join(LoggerActor.format_epoch(final, 100)) + "\n"
-            assert text.endswith(want)
+            # the reference's shape at size (6, 6): 13 dashes, 6 rows of 6 entries
+            want = "\n".join(LoggerActor.format_epoch(final, 100, size=(6, 6))) + "\n"
+            assert text.endswith(want) and want.split("\n")[1] == "-" * 13
+            assert want.count("[") == 6 and all(r.count(",") == 5 for r in want.split("\n") if r.startswith("["))
             (tmp_path / "info.log").unlink()
 
 
@@ -63,4 +65,17 @@ def test_frontend_reads_application_conf(gpu, tmp_path):
     final, want = O.run_packed(O.pack(cells), 11, 7, O.REF_CLIPPED, O.LIFE)
     got = [int(ln.split()[2], 16) for ln in p.stdout.splitlines() if ln.startswith("hash ")]
     assert got == [int(x) for x in want]
-    assert "\n".join(LoggerActor.format_epoch(O.unpack(final, 11), 7)) in p.stdout
+    assert "\n".join(LoggerActor.format_epoch(O.unpack(final, 11), 7, size=(10, 8))) in p.stdout
+
+
+def test_frontend_full_board_dump(gpu, tmp_path):
+    """log.full=true (this build's extension): every row and column of the
+    (x+1) x (y+1) board, 2(x+1)+1 dashes."""
+    entry = GOLDEN["ref_default"][0]
+    hashes, text = run([f"simulation.seed={entry['java_seed']}", "simulation.rule=life",
+                        "simulation.generations=100", "log.every=100", "log.full=true"], tmp_path)
+    res = entry["modes"]["life"]
+    assert hashes == res["hashes"]
+    final = np.array([[int(ch) for ch in row] for row in res["boards"][-1]["cells"]], dtype=np.uint8)
+    want = "\n".join(LoggerActor.format_epoch(final, 100)) + "\n"
+    assert text.endswith(want) and want.split("\n")[1] == "-" * 15

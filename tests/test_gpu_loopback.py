@@ -5,7 +5,7 @@ libgol's multi-rank exchange over RCCL ("the multi-rank RCCL
 issue order is asserted only in Python").  gol_comm_init_loopback joins
 contexts of one process -- one host thread each, as one process per GPU
 would be -- into a ring whose transport executes exactly the halo operation
-list one_pass hands to RCCL (gol_capi.cpp HaloOp: last rows -> down, first
+list one_pass hands to RCCL (gol_ring.cpp HaloOp: last rows -> down, first
 rows -> up, top halo <- up, bottom halo <- down), matched per (sender,
 receiver) pair in FIFO order like ncclSend / ncclRecv.  With N = 2 the up
 and down peers coincide, so a wrong issue order swaps the halos.  Checked

@@ -78,7 +78,7 @@ def test_rccl_ring_matches_oracle(gpu, world, topology, gpp):
 
 # --------------------------------------------------------------------------
 # 1-rank self-ring: the RCCL ring schedule on the box's single GPU.  A context
-# with a 1-rank communicator runs gol_capi.cpp one_pass's sharded branch
+# with a 1-rank communicator runs gol_ring.cpp one_pass's sharded branch
 # (interior rows || ncclSend/ncclRecv of G rows to itself, then the boundary
 # rows on the edge stream after the exchange event), so every depth and the
 # rows <= 2G path are checked against the oracle here, not only in the

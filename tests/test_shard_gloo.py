@@ -1,5 +1,5 @@
 """Multi-rank path on CPU (world_size 2 and 3, gloo): row-block shards that
-exchange halo rows exactly as libgol's RCCL ring does (gol_capi.cpp
+exchange halo rows exactly as libgol's RCCL ring does (gol_ring.cpp
 one_pass: before every pass of G generations, the last G rows down and the
 first G rows up, G-row halos back, in shard.HaloPlan's op order; the pass
 depth capped at floor(H / N), shard.ring_depth_cap) and reduce per-generation
