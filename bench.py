@@ -795,6 +795,25 @@ def rank_table(job, N, stats, dt, info):
     return job.gather(row)
 
 
+def drill_error_files(job):
+    """The files in which ranks whose fault drill raised left their exception
+    (fault_drill), for rank 0's watchdog."""
+    import glob
+    return sorted(glob.glob(glob.escape(job.uid_path("fault_error")) + ".r*"))
+
+
+def drill_errors(job):
+    """{rank: exception text} from drill_error_files."""
+    out = {}
+    for p in drill_error_files(job):
+        try:
+            with open(p) as f:
+                out[p.rsplit(".r", 1)[1]] = f.read()
+        except OSError:
+            pass
+    return out
+
+
 def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     """BASELINE.json configs[4] at N > 1, after the timed windows: the ranks
     lose rank min(3, N - 1) after generation 25 of 50 (checkpoints every 10)
@@ -831,6 +850,8 @@ def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     if job.rank == 0:
         shutil.rmtree(ckpt, ignore_errors=True)
         os.makedirs(ckpt)
+        for p in drill_error_files(job):  # a crashed earlier launch's reports
+            os.unlink(p)
     job.barrier()
     make = lambda r0, n: GolEngine(W, H, topology="torus", rule="life", device=local, row0=r0, rows=n)  # noqa: E731
     join = lambda e, tag, r, w: job.join(e, N, tag=tag, rank=r, world=w)  # noqa: E731
@@ -841,9 +862,23 @@ def fault_drill(job, N, GolEngine, eng, a, W, H, local, parity):
     except Exception as exc:  # noqa: BLE001 -- reported on the line; peers left in a collective meet the watchdog
         parity.checks.append({"what": "fault drill", "board": f"{W}x{H}", "error": repr(exc), "match": False})
         print(f"bench.py rank {job.rank}: fault drill failed: {exc!r}", file=sys.stderr, flush=True)
-        if job.rank == 0:
-            shutil.rmtree(ckpt, ignore_errors=True)
-        return ({"status": "error", "error": repr(exc)} if job.rank == 0 else None), None
+        # for rank 0's watchdog: its peers are now stuck in a collective this
+        # rank will never join, and the line should say why
+        try:
+            with open(f"{job.uid_path('fault_error')}.r{job.rank}", "w") as f:
+                f.write(repr(exc)[:2000])
+        except OSError:
+            pass
+        if job.rank != 0:
+            return None, None
+        shutil.rmtree(ckpt, ignore_errors=True)
+        rec = {"status": "error", "error": repr(exc)}
+        errs = {r: e for r, e in drill_errors(job).items() if r != "0"}
+        if errs:  # a peer raised first (rank 0's own error is then the broken collective)
+            rec["rank_errors"] = errs
+            parity.checks.append({"what": "fault drill (peers)", "board": f"{W}x{H}", "error": repr(errs),
+                                  "match": False})
+        return rec, None
     if eng is None:  # the lost rank: its context is gone, it sits out the rest
         return None, None
     nw, nr = rep["world_after"], job.rank if job.rank < rep["victim_rank"] else job.rank - 1
@@ -1052,10 +1087,15 @@ def main():
         def give_up():
             msg = f"fault drill did not finish within {a.fault_timeout:.0f} s"
             if rank == 0:
-                line = dict(line_before, fault_recovery={"status": "timed out", "timeout_s": a.fault_timeout,
-                                                          "note": "a rank that raised inside the drill reports "
-                                                                  "its exception on its own stderr"})
-                line["parity_failed"] = failed_before + [msg]
+                errs = drill_errors(job)
+                fr = {"status": "timed out", "timeout_s": a.fault_timeout,
+                      "note": "ranks whose drill raised (rank_errors) left their peers waiting in a collective; "
+                              "each also reports on its own stderr"}
+                if errs:
+                    fr["rank_errors"] = errs
+                line = dict(line_before, fault_recovery=fr)
+                line["parity_failed"] = failed_before + [msg] + [f"fault drill raised on rank {r}: {e}"
+                                                                 for r, e in sorted(errs.items())]
                 line["parity_ok"] = False
                 os.write(result_fd, (json.dumps(line) + "\n").encode())
             print(f"bench.py rank {rank}: {msg}", file=sys.stderr, flush=True)

@@ -243,6 +243,7 @@ def test_fault_drill_watchdog(tmp_path):
     assert d["value"] > 0 and d["parity"]["match"] is True  # the measured windows are intact
     fr = d["fault_recovery"]
     assert (fr["status"], fr["timeout_s"]) == ("timed out", 8.0) and "stderr" in fr["note"]
+    assert "rank_errors" not in fr  # a hang, not an exception
     # the line is the snapshot taken before the drill: none of its checks leaked in
     assert not any("fault drill" in c["what"] for c in d["parity"]["checks"])
     assert d["parity_ok"] is False and any("fault drill" in f for f in d["parity_failed"])
@@ -268,3 +269,18 @@ def test_fault_drill_error_on_rank0(tmp_path):
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert d["fault_recovery"]["status"] == "error" and "No space left" in d["fault_recovery"]["error"]
     assert d["value"] > 0 and d["parity_ok"] is False
+
+
+def test_fault_drill_error_on_a_peer(tmp_path):
+    """A drill that raises on a non-zero rank (its checkpoint write at epoch
+    20) leaves rank 0 in a collective the peer never joins: with RCCL it
+    waits for the watchdog, with the gloo stand-in the collective breaks when
+    the peer exits.  Either way rank 0's line names the peer's exception
+    under fault_recovery.rank_errors and fails parity."""
+    outs, _ = _run(3, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
+                   "--fault-timeout", "8", extra_env={"FAKE_DRILL_RAISE": "1"}, rc=None)
+    d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
+    fr = d["fault_recovery"]
+    assert fr["status"] in ("timed out", "error") and list(fr["rank_errors"]) == ["1"]
+    assert "No space left" in fr["rank_errors"]["1"]
+    assert d["parity_ok"] is False
