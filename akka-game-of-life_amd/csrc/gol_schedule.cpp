@@ -133,6 +133,29 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
     return (int)band;
 }
 
+// Small boards (round 6).  The rules above were measured on boards of
+// >= 65536 columns and rows, where a pass is at least one round of resident
+// waves.  On a small board they leave the GPU nearly empty -- a 4096^2 pass
+// of G = 10 in 256-row bands is 2 strips x 16 bands = 32 waves, each
+// streaming 276 rows through 10 stages one dependent instruction after the
+// other (14.4 us per generation).  When the chosen band gives fewer waves than
+// the GPU holds at once, the band is cut to about 1.5 rounds of resident waves
+// (rows x strips / (1.5 resident), a multiple of 4, >= 4 rows), trading the
+// taller bands' smaller halo share for parallelism.  Same-box sweep of depth x
+// band (scripts/small_sweep.py, profiles/r06_small_sweep.txt, us per
+// generation, unhashed): 4096^2 14.4 -> 2.3 at G = 10 in 4-row bands, 8192^2
+// 14.4 -> 3.1-3.3, 16384^2 14.3 -> 5.3, 32768^2 18.1 -> 11.9; G = 10 stays the
+// best depth (or within 3 % of it) at every size, hashed or not.  Returns the
+// band, or 0 when the board fills the GPU (the rules above stand).
+int small_board_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int band, int64_t resident) {
+    if (ctx->band_rows > 0 || gens <= 1 || resident <= 0 || strips <= 0 || band <= 0) return 0;
+    const int64_t waves = (rows + band - 1) / band * strips;
+    if (waves >= resident) return 0;
+    int64_t b = (2 * rows * strips + 3 * resident - 1) / (3 * resident);
+    b = std::max<int64_t>((b + 3) / 4 * 4, 4);
+    return (int)std::min<int64_t>(b, band);
+}
+
 // Tail split of a pass's rows (DESIGN.md §4 "Band schedule").  The
 // dispatcher hands workgroups to CUs as slots free up, so a pass of a few
 // rounds of resident waves ends with uneven per-SIMD tails: the CUs that got
@@ -300,14 +323,16 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     const bool clipped = ctx->topology == GOL_REF_CLIPPED;
     const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int64_t resident = (n == 1 && gens > 1) ? resident_waves(ctx, vec, gens, life, slots != nullptr, clipped) : 0;
-    const int band = pick_band(ctx, maxlen, p.strips, gens, resident);
+    int band = pick_band(ctx, maxlen, p.strips, gens, resident);
+    const int small = n == 1 ? small_board_band(ctx, maxlen, p.strips, gens, band, resident) : 0;
+    if (small > 0) band = small;
     int32_t rlo[2] = {0, 0}, rhi[2] = {0, 0}, rband[2] = {band, band};
     int nr = n;
     for (int k = 0; k < n; ++k) {
         rlo[k] = lo[k];
         rhi[k] = hi[k];
     }
-    if (n == 1 && gens > 1) {
+    if (n == 1 && gens > 1 && small == 0) {  // a small board's pass is ~1.5 rounds: no tail to even out
         const TailSplit t = tail_split(ctx, hi[0] - lo[0], p.strips, band, resident, gens);
         if (t.rows > 0) {  // bulk [lo, hi - t.rows) in `band` rows, tail in t.band rows
             nr = 2;

@@ -40,7 +40,7 @@ def test_board_creator_over_gpu_engine(gpu, entry, rule):
             got += bc.next_step()
         bc.log_every = 100  # logged when the step count is a multiple (BoardCreator.next_step)
         got += bc.next_step(96)  # a tick that has fallen behind: 96 generations in one call
-        assert bc.step == 100 and eng.epoch() == 100
+        assert bc.step == 100 and eng.epoch == 100
     assert got == [int(h) for h in res["hashes"]]
     want = []
     for e in (1, 2, 3, 4, 100):
