@@ -290,7 +290,13 @@ class Parity:
 
     def __init__(self):
         self.tables = {}
+        self.sources = {}  # shape -> the file a table came from, when not tests/golden/bench_*.json
         self.checks = []
+
+    def add_table(self, shape, hashes, source):
+        """A golden table (epoch k -> hash) from another committed file."""
+        self.tables[shape] = list(hashes)
+        self.sources[shape] = source
 
     def _golden(self, shape, epoch):
         if shape not in self.tables:
@@ -324,7 +330,7 @@ class Parity:
 
     def report(self):
         ms = [c["match"] for c in self.checks]
-        used = sorted(golden_path(*k) for k, v in self.tables.items() if v is not None)
+        used = sorted(self.sources.get(k, golden_path(*k)) for k, v in self.tables.items() if v is not None)
         return {"golden": (", ".join(used) + " (CPU oracle, tests/golden/make_bench_golden.py; "
                            "parity unpinned: the reference ships no vectors)") if used else None,
                 "checks": self.checks,
@@ -705,6 +711,64 @@ def secondary_run(GolEngine, a, local, parity=None):
     return out
 
 
+SMALL_EDGE, SMALL_GENS = 4096, 1000
+
+
+def golden_small():
+    """tests/golden/golden.json's 4096^2 torus (seed 0x5EED, B3/S23): the
+    hashes at epochs 0..1000, or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            for ent in json.load(f)["torus"]:
+                if (ent["W"], ent["H"], ent["seed"], ent["rule"]) == (SMALL_EDGE, SMALL_EDGE, GOLDEN_SEED, "life"):
+                    return [int(ent["hash0"])] + [int(h) for h in ent["hashes"]]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def small_board_run(GolEngine, local, parity):
+    """BASELINE.json configs[1]: the 4096^2 torus for 1000 generations (2 MiB
+    per plane: the board lives in the caches, so the pass is bound by the
+    latency of each wave's row stream, not by HBM -- gol_schedule.cpp
+    small_board_band).  One untimed run from the seed (code-object and clock
+    warm-up), then timed from the seed again: unhashed, then with every
+    generation's hash, each checked against tests/golden/golden.json."""
+    S, n = SMALL_EDGE, SMALL_GENS
+    shape = (S, S)
+    g = golden_small()
+    if g is not None and parity is not None:
+        parity.add_table(shape, g, "tests/golden/golden.json (torus 4096^2, seed 0x5EED)")
+    out = {"workload": f"{S}x{S} torus B3/S23, {n} generations from the seed (BASELINE.json configs[1])"}
+    with GolEngine(S, S, topology="torus", rule="life", device=local) as e:
+        for hashed in (False, True):
+            e.seed(GOLDEN_SEED)
+            e.step(n, hashes=hashed)
+            e.sync()
+            e.seed(GOLDEN_SEED)
+            e.sync()
+            e.profile(True)
+            e.profile_reset()
+            t0 = time.perf_counter()
+            hs = e.step(n, hashes=hashed)
+            e.sync()
+            dt = time.perf_counter() - t0
+            kms, launches, _ = e.profile_read()
+            e.profile(False)
+            rec = {"value": round(S * S * n / dt / 1e9, 1), "unit": "GCUPS", "wall_ms": round(dt * 1e3, 3),
+                   "kernel_ms": round(kms, 3), "launches": launches, "pass_plan": compact_plan(e.pass_plan(n, hashed))}
+            if parity is not None:
+                rec["parity"] = parity.board(f"configs[1] 4096^2 x {n}{' hashed' if hashed else ''}: gol_hash after "
+                                             f"{n}", shape, n, e.hash())
+                if hashed:
+                    seq = parity.sequence(f"configs[1] 4096^2: the {n} fused per-generation hashes", shape, 1, hs)
+                    rec["parity_per_generation"] = {k: seq[k] for k in ("checked", "mismatched_epochs", "match")}
+            out["with_state_hash" if hashed else "unhashed"] = rec
+    out["value"] = out["unhashed"]["value"]
+    out["unit"] = "GCUPS"
+    return out
+
+
 def ring_stats(st, passes):
     """The self-ring windows' exchange figures (gol_profile_stats_read)."""
     n = max(st["exchanges"], 1)
@@ -956,6 +1020,7 @@ def main():
     secondary = None
     if world == 1 and not a.no_secondary:
         secondary = secondary_run(GolEngine, a, local, parity)
+        secondary["configs1_4096"] = small_board_run(GolEngine, local, parity)
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
     eng.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)

@@ -34,6 +34,10 @@ M64 = (1 << 64) - 1
 
 
 def golden(width, height):
+    if (width, height) == (4096, 4096):  # configs[1]'s table lives in golden.json
+        with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+            ent = next(e for e in json.load(f)["torus"] if (e["W"], e["H"], e["seed"]) == (4096, 4096, 0x5EED))
+        return [int(ent["hash0"])] + [int(h) for h in ent["hashes"]]
     name = f"bench_{width}.json" if width == height else f"bench_{width}x{height}.json"
     with open(os.path.join(ROOT, "tests", "golden", name)) as f:
         return [int(x, 16) for x in json.load(f)["hashes"]]

@@ -137,6 +137,10 @@ def test_single_rank_keeps_cpu_baseline_slot(tmp_path):
     outs, logs = _run(1, tmp_path, "--steps", "12", "--warmup", "2", "--no-cpu", "--no-ring")
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     assert d["n_gpus"] == 1 and d["value"] > 0 and "note" not in d["secondary"]
+    c1 = d["secondary"]["configs1_4096"]  # BASELINE.json configs[1], checked against golden.json
+    assert c1["value"] > 0 and c1["unhashed"]["parity"]["match"] is True
+    assert c1["with_state_hash"]["parity_per_generation"] == {"checked": 1000, "mismatched_epochs": [], "match": True}
+    assert "tests/golden/golden.json" in d["parity"]["golden"]
     assert d["parity"]["match"] is True
     assert [c.get("epoch") for c in d["parity"]["checks"] if c["board"] == "262144x262144"][0] == 14
     assert "ranks" not in d and d["runtime"]["torch_loaded"] is False
@@ -158,7 +162,7 @@ def test_single_rank_ring_windows_carry_parity(tmp_path):
         assert ring[k]["parity"]["epoch"] == 25 and ring[k]["parity"]["match"] is True, k
     assert ring["per_rank_shard_self_ring"]["exchange"]["passes"] >= 1
     boards = {c["board"] for c in d["parity"]["checks"]}
-    assert boards == {"65536x65536", "262144x262144", "262144x32768"}
+    assert boards == {"4096x4096", "65536x65536", "262144x262144", "262144x32768"}
     assert d["parity"]["match"] is True
 
 
