@@ -1,9 +1,10 @@
 """CPU: the JNI glue a JVM backend binds (bindings/jni/gol_jni.c) stays in
 step with include/gol.h and with its Scala declarations
-(bindings/jni/GolNative.scala).  Syntax-checked, no JVM run: the image has no
-JDK, so it compiles with gcc -fsyntax-only -Werror against
-bindings/jni/jni_min/jni.h (a JNI subset for this check only) -- a changed
-gol.h signature the glue calls breaks this test."""
+(bindings/jni/GolNative.scala).  No JVM: the image has no JDK, so it compiles
+with gcc -fsyntax-only -Werror against bindings/jni/jni_min/jni.h (a JNI
+subset for this check only) -- a changed gol.h signature the glue calls breaks
+this test; tests/test_gpu_jni_stub.py runs it on the GPU through a stub
+JNIEnv."""
 import os
 import re
 import shutil
