@@ -511,10 +511,9 @@ int gol_set_tuning(gol_ctx* ctx, int32_t band_rows, int32_t gens_per_pass, int32
     ctx->vec_fixed = words_per_lane;
     // a new lane width selects other instances: load them now, not inside the
     // caller's first (timed) step
-    if (lanes_changed) {
+    if (lanes_changed) {  // the occupancy queries load the code objects; nothing to wait for on the device
         if (int rc = bind(ctx)) return rc;
         preload_instances(ctx);
-        HIP_CHECK(ctx, hipDeviceSynchronize());
     }
     return GOL_OK;
 }
