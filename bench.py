@@ -769,6 +769,60 @@ def small_board_run(GolEngine, local, parity):
     return out
 
 
+AKKA_DEFAULT_SEED = 42  # tests/golden/golden.json ref_default entry (java.util.Random seed)
+
+
+def default_board_run(GolEngine, local, parity):
+    """BASELINE.json configs[0] on this engine: the reference's own default
+    board -- size (6, 6), i.e. 7 x 7 cells with neighbours clipped to
+    [0, 6) x [0, 6) (application.conf:31-33, package.scala:17-28) -- from the
+    java.util.Random(42) board of BoardCreator.scala:23 (the golden vectors'
+    initial cells, a data file), 100 generations of the rule the reference
+    actually runs (ref-effective: the identity) and of B3/S23.  Timed as the
+    reference drives it -- one gol_step(1) per NextStep tick
+    (BoardCreator.scala:113-116) -- and as one call; every generation's hash
+    against golden.json.  The Akka cluster itself cannot run here (no JVM):
+    its ceiling is one generation per 3000 ms tick (cpu_baseline)."""
+    import numpy as np
+    from gameoflife import codec
+    with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+        ent = next(e for e in json.load(f)["ref_default"] if e["java_seed"] == AKKA_DEFAULT_SEED)
+    x, y = ent["w"], ent["h"]
+    cells = np.array([[int(c) for c in r] for r in ent["initial"]], dtype=np.uint8)
+    out = {"workload": f"the reference's default board: size ({x}, {y}) = {x + 1}x{y + 1} cells, ref-clipped, "
+                       f"java.util.Random({AKKA_DEFAULT_SEED}) initial board, 100 generations (BASELINE.json configs[0])"}
+    for rule in ("ref-effective", "life"):
+        want = [int(h) for h in ent["modes"][rule]["hashes"]]
+        n = len(want)
+        with GolEngine(x + 1, y + 1, topology="ref-clipped", rule=rule, device=local) as e:
+            e.load(codec.pack(cells))
+            e.step(n)  # code-object / first-call warm-up
+            res = {}
+            for mode in ("per_tick", "one_call"):
+                e.load(codec.pack(cells))
+                e.sync()
+                t0 = time.perf_counter()
+                if mode == "per_tick":
+                    hs = np.concatenate([e.step(1, hashes=True) for _ in range(n)])
+                else:
+                    hs = e.step(n, hashes=True)
+                e.sync()
+                dt = time.perf_counter() - t0
+                ok = [int(h) for h in hs] == want
+                if parity is not None:
+                    parity.checks.append({"what": f"configs[0] default board, {rule}, {mode}: the {n} per-generation "
+                                                  "hashes", "board": f"{x + 1}x{y + 1}", "epochs": [1, n],
+                                          "checked": n, "match": ok})
+                res[mode] = {"us_per_generation": round(dt / n * 1e6, 2),
+                             "generations_per_s": round(n / dt), "parity": ok,
+                             "vs_akka_tick": round(AKKA_TICK_S / (dt / n)),
+                             }
+            out[rule] = res
+    out["note"] = ("vs_akka_tick: the reference's 3000 ms per generation (application.conf:40) over this engine's time "
+                   "per generation on the same board; the Akka run itself is not measurable here (no JVM)")
+    return out
+
+
 def ring_stats(st, passes):
     """The self-ring windows' exchange figures (gol_profile_stats_read)."""
     n = max(st["exchanges"], 1)
@@ -1021,6 +1075,7 @@ def main():
     if world == 1 and not a.no_secondary:
         secondary = secondary_run(GolEngine, a, local, parity)
         secondary["configs1_4096"] = small_board_run(GolEngine, local, parity)
+        secondary["configs0_default_board"] = default_board_run(GolEngine, local, parity)
     row0, rows = N.shard_rows(H, rank, world)
     eng = GolEngine(W, H, topology="torus", rule="life", device=local, row0=row0, rows=rows)
     eng.set_tuning(band_rows=a.band, gens_per_pass=a.gpp)

@@ -109,10 +109,17 @@ class FakeEngine:
         world = int(os.environ.get("WORLD_SIZE", "1"))
         # in a multi-rank job a shard is rows of the global torus; alone, a
         # context with fewer rows is a torus of its own height (as libgol's)
-        self.board = FakeBoard(width, height if world > 1 else self.rows)
+        self.board = FakeBoard(width, height if world > 1 else self.rows) if topology == "torus" else None
         if world == 1:
             self.row0 = 0
         self.corrupt = os.environ.get("FAKE_CORRUPT_RANK") == str(RANK)
+        # the reference's default 7 x 7 board (bench.py default_board_run):
+        # its per-generation hashes come from golden.json's ref_default entry
+        self.ref_default = None
+        if topology == "ref-clipped":
+            with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+                ent = next(e for e in json.load(f)["ref_default"] if e["java_seed"] == 42)
+            self.ref_default = [int(h) for h in ent["modes"][rule]["hashes"]]
         log("create", f"{width}x{self.rows}", "device", device, "row0", row0)
 
     def _hash(self, epoch):
@@ -171,7 +178,15 @@ class FakeEngine:
         plan = [12] * (n // 12)
         return plan + [n % 12] if n % 12 else plan
 
+    def load(self, packed):
+        self.epoch = 0
+        log("load", f"{self.w}x{self.rows}")
+
     def step(self, n, hashes=False):
+        if self.ref_default is not None:
+            e0 = self.epoch
+            self.epoch += n
+            return np.array(self.ref_default[e0:e0 + n], dtype=np.uint64) if hashes else None
         plan = self.pass_plan(n, hashes)
         self.gens += n
         self.launches += len(plan)

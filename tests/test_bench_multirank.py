@@ -141,6 +141,10 @@ def test_single_rank_keeps_cpu_baseline_slot(tmp_path):
     assert c1["value"] > 0 and c1["unhashed"]["parity"]["match"] is True
     assert c1["with_state_hash"]["parity_per_generation"] == {"checked": 1000, "mismatched_epochs": [], "match": True}
     assert "tests/golden/golden.json" in d["parity"]["golden"]
+    c0 = d["secondary"]["configs0_default_board"]  # BASELINE.json configs[0]'s board on this engine
+    for rule in ("ref-effective", "life"):
+        for mode in ("per_tick", "one_call"):
+            assert c0[rule][mode]["parity"] is True and c0[rule][mode]["vs_akka_tick"] > 0
     assert d["parity"]["match"] is True
     assert [c.get("epoch") for c in d["parity"]["checks"] if c["board"] == "262144x262144"][0] == 14
     assert "ranks" not in d and d["runtime"]["torch_loaded"] is False
@@ -162,7 +166,7 @@ def test_single_rank_ring_windows_carry_parity(tmp_path):
         assert ring[k]["parity"]["epoch"] == 25 and ring[k]["parity"]["match"] is True, k
     assert ring["per_rank_shard_self_ring"]["exchange"]["passes"] >= 1
     boards = {c["board"] for c in d["parity"]["checks"]}
-    assert boards == {"4096x4096", "65536x65536", "262144x262144", "262144x32768"}
+    assert boards == {"7x7", "4096x4096", "65536x65536", "262144x262144", "262144x32768"}
     assert d["parity"]["match"] is True
 
 
