@@ -283,12 +283,13 @@ def test_fault_drill_error_on_a_peer(tmp_path):
     """A drill that raises on a non-zero rank (its checkpoint write at epoch
     20) leaves rank 0 in a collective the peer never joins: with RCCL it
     waits for the watchdog, with the gloo stand-in the collective breaks when
-    the peer exits.  Either way rank 0's line names the peer's exception
+    the peer exits (and a third rank's collective may break with it, so it
+    can be named too).  Either way rank 0's line names the peer's exception
     under fault_recovery.rank_errors and fails parity."""
     outs, _ = _run(3, tmp_path, "--steps", "20", "--warmup", "5", "--no-cpu", "--no-secondary",
                    "--fault-timeout", "8", extra_env={"FAKE_DRILL_RAISE": "1"}, rc=None)
     d = json.loads([ln for ln in outs[0].splitlines() if ln.strip()][0])
     fr = d["fault_recovery"]
-    assert fr["status"] in ("timed out", "error") and list(fr["rank_errors"]) == ["1"]
+    assert fr["status"] in ("timed out", "error") and "1" in fr["rank_errors"] and "0" not in fr["rank_errors"]
     assert "No space left" in fr["rank_errors"]["1"]
     assert d["parity_ok"] is False
