@@ -145,6 +145,7 @@ void destroy_impl(gol_ctx* c) {
     for (void* p : {(void*)c->snap, (void*)c->clk_buf, (void*)c->plane[0], (void*)c->plane[1], (void*)c->halo_top,
                     (void*)c->halo_bot, (void*)c->zero_row, (void*)c->slots})
         if (p) hip_note(hipFree(p), "destroy: hipFree");
+    if (c->host_slots) hip_note(hipHostFree(c->host_slots), "destroy: hipHostFree");
     for (hipStream_t st : {c->compute, c->comm, c->edge, c->xfer})
         if (st) hip_note(hipStreamDestroy(st), "destroy: hipStreamDestroy");
     delete c;
@@ -389,7 +390,7 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
             if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
             g += (uint32_t)G;
         }
-        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, n * per * sizeof(unsigned long long),
+        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, n * per * sizeof(unsigned long long),
                                       hipMemcpyDeviceToHost, ctx->compute));
         HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
         fold_slots(ctx, n, hashes_out + g0);
@@ -427,7 +428,7 @@ int gol_hash(gol_ctx* ctx, uint64_t* hash_out) {
     HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, per * sizeof(unsigned long long), ctx->compute));
     HIP_CHECK(ctx, gol::launch_hash(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
                                     ctx->ilv, ctx->slots, ctx->compute));
-    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, per * sizeof(unsigned long long),
+    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, per * sizeof(unsigned long long),
                                   hipMemcpyDeviceToHost, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
     fold_slots(ctx, 1, hash_out);

@@ -112,7 +112,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     e = hipMemcpyAsync(ctx->plane[ctx->cur], blk[cur] + n * pitch, (size_t)ctx->rows * pitch * 4,
                        hipMemcpyDeviceToDevice, ctx->compute);
     if (e == hipSuccess && hashes_out)
-        e = hipMemcpyAsync(ctx->host_slots.data(), ctx->slots, (size_t)n * gol::kHashGenStride * 8,
+        e = hipMemcpyAsync(ctx->host_slots, ctx->slots, (size_t)n * gol::kHashGenStride * 8,
                            hipMemcpyDeviceToHost, ctx->compute);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->compute);
     if (e != hipSuccess) return fail_hip(e, "light-cone result");

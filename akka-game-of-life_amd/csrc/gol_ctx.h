@@ -80,7 +80,8 @@ struct gol_ctx {
     uint32_t* zero_row = nullptr;
     unsigned long long* slots = nullptr;  // [gens][kHashSlots * kHashSlotStride]
     uint32_t slots_gens = 0;
-    std::vector<unsigned long long> host_slots;
+    unsigned long long* host_slots = nullptr;  // page-locked copy of `slots` (hipHostMalloc: the per-generation
+                                               // readback is a direct DMA, not a staged pageable copy)
     uint64_t epoch = 0;
     hipStream_t compute = nullptr, comm = nullptr;
     hipStream_t edge = nullptr;  // boundary-row kernels of a sharded pass (concurrent with the interior)

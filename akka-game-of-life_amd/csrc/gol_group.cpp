@@ -192,7 +192,7 @@ int gol_group_step_partials(gol_group* g, uint32_t generations, uint64_t* hashes
             for (int k = 0; k < n; ++k) {
                 gol_ctx* s = g->shards[k];
                 if (int rc = bind(s)) return group_fail(g, s, rc);
-                hipError_t e = hipMemcpyAsync(s->host_slots.data(), s->slots, cnt * per * sizeof(unsigned long long),
+                hipError_t e = hipMemcpyAsync(s->host_slots, s->slots, cnt * per * sizeof(unsigned long long),
                                               hipMemcpyDeviceToHost, s->compute);
                 if (e == hipSuccess) e = hipStreamSynchronize(s->compute);
                 if (e != hipSuccess) return group_fail(g, s, hip_fail(s, e, "hash readback", __FILE__, __LINE__));

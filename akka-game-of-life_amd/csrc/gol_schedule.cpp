@@ -238,9 +238,12 @@ int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     if (ctx->slots) HIP_CHECK(ctx, hipFree(ctx->slots));
     ctx->slots = nullptr;
     const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
+    ctx->slots_gens = 0;
     HIP_CHECK(ctx, hipMalloc(&ctx->slots, n * sizeof(unsigned long long)));
-    ctx->slots_gens = gens;
-    ctx->host_slots.resize(n);
+    if (ctx->host_slots) HIP_CHECK(ctx, hipHostFree(ctx->host_slots));
+    ctx->host_slots = nullptr;
+    HIP_CHECK(ctx, hipHostMalloc((void**)&ctx->host_slots, n * sizeof(unsigned long long), hipHostMallocDefault));
+    ctx->slots_gens = gens;  // only once both buffers exist
     return GOL_OK;
 }
 
@@ -249,7 +252,7 @@ void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out) {
     for (uint32_t g = 0; g < gens; ++g) {
         uint64_t h = 0;
         const unsigned long long* s =
-            ctx->host_slots.data() + (size_t)g * gol::kHashSlots * gol::kHashSlotStride;
+            ctx->host_slots + (size_t)g * gol::kHashSlots * gol::kHashSlotStride;
         for (int k = 0; k < gol::kHashSlots; ++k) h += s[(size_t)k * gol::kHashSlotStride];
         out[g] = h;
     }
