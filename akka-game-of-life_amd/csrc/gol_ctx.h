@@ -122,7 +122,7 @@ struct gol_ctx {
     uint64_t halo_sent = 0, halo_recv = 0;             // bytes posted to the ring since the last reset
     // occupancy
     int num_cus = 0;
-    std::map<int, int64_t> occupancy_cache;
+    mutable std::map<int, int64_t> occupancy_cache;  // resident_waves (a cache: const callers may fill it)
     std::string err;
 };
 
@@ -180,7 +180,7 @@ void destroy_impl(gol_ctx* c);
 int ensure_slots(gol_ctx* ctx, uint32_t gens);
 void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out);
 int lane_words(const gol_ctx* ctx, int gens);
-int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped);
+int64_t resident_waves(const gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped);
 // Load every step kernel instance the context can launch at its current
 // tuning (the occupancy query of an instance loads its code object).
 void preload_instances(gol_ctx* ctx);

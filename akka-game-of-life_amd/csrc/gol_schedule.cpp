@@ -275,7 +275,7 @@ int lane_words(const gol_ctx* ctx, int gens) {
 }
 
 // Resident waves on the whole GPU for a launch (cached occupancy query).
-int64_t resident_waves(gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
+int64_t resident_waves(const gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped) {
     const int key = ((((vec * 16 + gens) * 2 + (life ? 1 : 0)) * 2 + (hash ? 1 : 0)) * 2 + (clipped ? 1 : 0)) * 8 +
                     ctx->ilv;
     auto it = ctx->occupancy_cache.find(key);
@@ -452,6 +452,25 @@ int depth_cap(const gol_ctx* ctx) {
     return (int)std::max<int64_t>(G, 1);
 }
 
+// A B3/S23 torus stepped whole (no ring, no group) whose 10-generation
+// passes fall under small_board_band.  There the hashed passes follow the
+// unhashed cost row: the hashed narrow row (measured at 65536^2) ties G = 7
+// with G = 10, but on small boards a launch costs nearly the same at any
+// depth and G = 7 runs 1.4 x the launches.  Same-box sweep, 1000 generations,
+// hashed, us per generation, G = 7 / 10 (scripts/small_depth.py,
+// profiles/r06_small_depth.txt): 1024^2 2.99 / 2.72, 4096^2 3.27 / 2.96,
+// 8192^2 5.15 / 4.08, 16384^2 6.97 / 7.08, 32768^2 15.33 / 15.33.
+static bool small_board(const gol_ctx* ctx) {
+    if (sharded(ctx) || ctx->group || !life_torus(ctx) || depth_cap(ctx) < 10) return false;
+    const int G = 10;
+    const int vec = lane_words(ctx, G);
+    const int sw = gol::strip_words(vec, G);
+    const int strips = (int)((ctx->wwords + sw - 1) / sw);
+    const int64_t resident = resident_waves(ctx, vec, G, true, true, false);
+    const int band = pick_band(ctx, ctx->rows, strips, G, resident);
+    return small_board_band(ctx, ctx->rows, strips, G, band, resident) > 0;
+}
+
 // Depths of the passes that advance `n` generations.  A fixed
 // gens_per_pass (tuning) is taken literally (the last pass shorter);
 // otherwise the plan minimises the summed pass cost (a DP over n, n <= 1024:
@@ -468,7 +487,7 @@ std::vector<int> plan_passes(const gol_ctx* ctx, uint32_t n, bool hashed) {
     }
     const int sw = gol::strip_words(lane_words(ctx, 6), 6);
     const bool wide = (ctx->wwords + sw - 1) / sw >= 32;
-    const double* cost = kPassCost[hashed ? 1 : 0][wide ? 1 : 0];
+    const double* cost = kPassCost[hashed && !small_board(ctx) ? 1 : 0][wide ? 1 : 0];
     std::vector<double> best(n + 1, 0.0);
     std::vector<int> pick(n + 1, 1);
     for (uint32_t k = 1; k <= n; ++k) {

@@ -385,6 +385,10 @@ def test_pass_plan(gpu):
         assert sum(check) == 13
     with engine(262144, 64, rule=rule_obj(O.REF_EFFECTIVE)) as e:  # other rules: planned passes stop at 8
         assert max(e.pass_plan(60)) <= 8 and sum(e.pass_plan(60)) == 60
+    with engine(4096, 4096) as e:  # small board (configs[1]): hashed passes plan like unhashed ones
+        assert e.pass_plan(1000, hashes=True) == [10] * 100 == e.pass_plan(1000)
+    with engine(65536, 65536) as e:  # fills the GPU: the hashed narrow row's G = 7 tie stands
+        assert 7 in e.pass_plan(1000, hashes=True)
 
 
 def test_snapshot_into_caller_buffer(gpu):
