@@ -745,18 +745,25 @@ def small_board_run(GolEngine, local, parity):
             e.seed(GOLDEN_SEED)
             e.step(n, hashes=hashed)
             e.sync()
+            # kernel time: a profiled run (events around every launch)
             e.seed(GOLDEN_SEED)
             e.sync()
             e.profile(True)
             e.profile_reset()
+            e.step(n, hashes=hashed)
+            e.sync()
+            kms, launches, _ = e.profile_read()
+            e.profile(False)
+            # wall time: the same run without the profiling events
+            e.seed(GOLDEN_SEED)
+            e.sync()
             t0 = time.perf_counter()
             hs = e.step(n, hashes=hashed)
             e.sync()
             dt = time.perf_counter() - t0
-            kms, launches, _ = e.profile_read()
-            e.profile(False)
             rec = {"value": round(S * S * n / dt / 1e9, 1), "unit": "GCUPS", "wall_ms": round(dt * 1e3, 3),
-                   "kernel_ms": round(kms, 3), "launches": launches, "pass_plan": compact_plan(e.pass_plan(n, hashed))}
+                   "kernel_ms": round(kms, 3), "kernel_ms_source": "a separate profiled run of the same generations",
+                   "launches": launches, "pass_plan": compact_plan(e.pass_plan(n, hashed))}
             if parity is not None:
                 rec["parity"] = parity.board(f"configs[1] 4096^2 x {n}{' hashed' if hashed else ''}: gol_hash after "
                                              f"{n}", shape, n, e.hash())
