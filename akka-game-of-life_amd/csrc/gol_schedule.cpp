@@ -161,19 +161,21 @@ int small_board_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int
 // rounds of resident waves ends with uneven per-SIMD tails: the CUs that got
 // the last full-height bands finish late.  The last `frac` x resident waves
 // therefore cover their rows in bands of band / div, dispatched after the
-// bulk.  Default: one resident round's worth of waves in bands of band / 3
-// (profiles/r01_tail_sweep.txt, reseeded boards, min of 4 rounds: +4 % on the
-// N = 8 per-rank shape 262144 x 32768, +2 % at x 65536, +1 % at x 131072 and
-// 262144^2; neutral to -3.6 % at 65536^2, so boards of < 32 strips keep one
-// band height).  GOL_TAIL="frac,div" overrides it (A/B
-// sweeps, scripts/tail_sweep.py); frac 0 disables it.
+// bulk.  Default: one resident round's worth of waves in bands of band / 4.
+// Round 1 chose band / 3 (profiles/r01_tail_sweep.txt: +4 % on the N = 8
+// per-rank shape 262144 x 32768, +2 % at x 65536, +1 % at x 131072 and
+// 262144^2).  Round 6 re-swept the divisor on the paired G = 10 kernels,
+// scored per probed GHz (scripts/band_scan.py, profiles/r06_tail/), band / 4
+// against band / 3: 262144^2 +1.6 % (hashed +1.8 %), 65536^2 +4.0 % (hashed
+// +0.3 %), 131072^2 and 262144 x 32768 +0.2 %, 262144^2 at G = 12 -0.3 %.
+// GOL_TAIL="frac,div" overrides it (A/B sweeps); frac 0 disables it.
 struct TailSplit {
     int32_t rows = 0;  // rows at the end of the range in short bands (0: none)
     int32_t band = 0;
 };
 
 constexpr double kTailFrac = 1.0;
-constexpr int kTailDiv = 3;
+constexpr int kTailDiv = 4;
 
 TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int64_t resident, int gens) {
     double frac = kTailFrac;
