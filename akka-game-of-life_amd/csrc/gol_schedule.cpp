@@ -161,13 +161,16 @@ int small_board_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int
 // rounds of resident waves ends with uneven per-SIMD tails: the CUs that got
 // the last full-height bands finish late.  The last `frac` x resident waves
 // therefore cover their rows in bands of band / div, dispatched after the
-// bulk.  Default: one resident round's worth of waves in bands of band / 4.
-// Round 1 chose band / 3 (profiles/r01_tail_sweep.txt: +4 % on the N = 8
-// per-rank shape 262144 x 32768, +2 % at x 65536, +1 % at x 131072 and
-// 262144^2).  Round 6 re-swept the divisor on the paired G = 10 kernels,
-// scored per probed GHz (scripts/band_scan.py, profiles/r06_tail/), band / 4
-// against band / 3: 262144^2 +1.6 % (hashed +1.8 %), 65536^2 +4.0 % (hashed
-// +0.3 %), 131072^2 and 262144 x 32768 +0.2 %, 262144^2 at G = 12 -0.3 %.
+// bulk.  Default: one resident round's worth of waves in bands of band / 4
+// for tall (>= 768-row) bands, band / 6 below.  Round 1 chose band / 3
+// (profiles/r01_tail_sweep.txt: +4 % on the N = 8 per-rank shape 262144 x
+// 32768, +2 % at x 65536, +1 % at x 131072 and 262144^2).  Round 6 re-swept
+// the divisor on the paired G = 10 kernels, scored per probed GHz
+// (scripts/band_scan.py, profiles/r06_tail/; tail1_* and tail2_* against /3,
+// tail3_* against /4).  /4 over /3: 262144^2 (1024-row bands) +1.6 %, hashed
+// +1.8 %; 65536^2 (256) +4.0 %; 262144^2 at G = 12 -0.3 %.  /6 over /4:
+// 131072^2 (384) +2.4 %, 262144 x 32768 (256) +2.4 %, hashed +2.9 %,
+// 262144 x 65536 (384) +0.2 %, 65536^2 -0.1 %, 262144^2 -3.6 %.
 // GOL_TAIL="frac,div" overrides it (A/B sweeps); frac 0 disables it.
 struct TailSplit {
     int32_t rows = 0;  // rows at the end of the range in short bands (0: none)
@@ -175,11 +178,13 @@ struct TailSplit {
 };
 
 constexpr double kTailFrac = 1.0;
-constexpr int kTailDiv = 4;
+constexpr int kTailDiv = 6;
+constexpr int kTailDivTall = 4;  // bands of >= kTailTallBand rows
+constexpr int kTailTallBand = 768;
 
 TailSplit tail_split(const gol_ctx* ctx, int64_t rows, int strips, int band, int64_t resident, int gens) {
     double frac = kTailFrac;
-    int div = kTailDiv;
+    int div = band >= kTailTallBand ? kTailDivTall : kTailDiv;
     const char* env = getenv("GOL_TAIL");
     if (env && *env) {
         if (sscanf(env, "%lf,%d", &frac, &div) != 2) frac = 0.0;
