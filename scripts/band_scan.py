@@ -5,7 +5,8 @@ and over a run; the per-GHz rate does not).
 
     python scripts/band_scan.py [EDGE|WxH] [G] [GENS] [TAILS] [h]
 GOL_TAIL="frac,div" forces the tail split (gol_schedule.cpp tail_split);
-TAILS ("f,d;f,d;...") scans only those, at the automatic band; "h" times the
+TAILS ("f,d;B@f,d;B@-;...") scans only those, at the automatic band or at
+band B (with that tail, or none); "h" times the
 hashed passes.
 """
 import os
@@ -26,7 +27,9 @@ def main():
     hashed = len(sys.argv) > 5 and sys.argv[5] == "h"
     cfgs = [(0, None)]
     if len(sys.argv) > 4 and sys.argv[4]:
-        cfgs += [(0, t) for t in sys.argv[4].split(";")]
+        for t in sys.argv[4].split(";"):  # "f,d" at the automatic band, or "B@f,d" / "B@-" at a fixed one
+            b, _, t = t.rpartition("@")
+            cfgs.append((int(b) if b else 0, None if t == "-" else t))
     else:
         cfgs += [(0, t) for t in ("0", "0.5,3", "1,2", "1,4", "2,3")]
         cfgs += [(b, None) for b in (192, 256, 320, 384, 448, 512, 768)]
