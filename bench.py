@@ -599,6 +599,9 @@ def roofline(kms, launches, gens_covered, cells, plan, shape, mode, hashed=False
         peak_held, _ = valu_peak_gcups(mix, clock)
         held.update({"ghz": round(clock, 3), "peak_at_held_clock": round(peak_held, 1),
                      "issue_efficiency": round(gcups / peak_held, 4),
+                     # the rate per held GHz: flat across boxes whose power limit holds
+                     # different clocks (profiles/r06_size_scan.txt)
+                     "gcups_per_ghz": round(gcups / clock, 1),
                      "source": "in-kernel probe of these timed launches: every sampled workgroup's core-clock "
                                "(s_memtime) and 100 MHz reference (s_memrealtime) ticks, summed (gol_profile_clock)"})
     r["held_clock"] = held
