@@ -242,13 +242,16 @@ int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     // a hipFree + hipMalloc between two hashed calls would synchronise the
     // device inside the caller's step
     gens = std::max<uint32_t>(gens, 1024);
-    if (ctx->slots) HIP_CHECK(ctx, hipFree(ctx->slots));
-    ctx->slots = nullptr;
-    const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
+    // the context forgets both buffers before freeing them, so a failure on
+    // the way leaves nothing to free twice (destroy_impl frees what is set)
     ctx->slots_gens = 0;
+    unsigned long long* old_dev = ctx->slots;
+    unsigned long long* old_host = ctx->host_slots;
+    ctx->slots = ctx->host_slots = nullptr;
+    if (old_dev) HIP_CHECK(ctx, hipFree(old_dev));
+    if (old_host) HIP_CHECK(ctx, hipHostFree(old_host));
+    const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
     HIP_CHECK(ctx, hipMalloc(&ctx->slots, n * sizeof(unsigned long long)));
-    if (ctx->host_slots) HIP_CHECK(ctx, hipHostFree(ctx->host_slots));
-    ctx->host_slots = nullptr;
     HIP_CHECK(ctx, hipHostMalloc((void**)&ctx->host_slots, n * sizeof(unsigned long long), hipHostMallocDefault));
     ctx->slots_gens = gens;  // only once both buffers exist
     return GOL_OK;
