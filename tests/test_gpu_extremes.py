@@ -10,7 +10,10 @@ oracle (bit-exact boards and every generation's hash).
 * a clipped board of 2^20 + 5 columns (a partial last word) and 40 rows;
 * the small-board band rule's smallest bands (gol_schedule.cpp
   small_board_band) on tori of 1 and 2 strips, at every depth the planner
-  picks and a few fixed ones.
+  picks and a few fixed ones;
+* the tail split (gol_schedule.cpp tail_split: the last round of resident
+  waves in bands of band / 6 below 768-row bands) on boards of an odd row
+  count, so the bulk range ends in a partial band before the tail bands.
 The planner chooses the depths unless a test fixes them."""
 import numpy as np
 import pytest
@@ -61,3 +64,10 @@ def test_wide_clipped_board_with_partial_word(gpu):
 def test_small_board_bands(gpu, S, gpp):
     """3968 columns = 62 pairs: exactly one strip; 4096 = 62 + 2 pairs."""
     _run(S, S // 4, 26, gpp=gpp, seed=S + gpp)
+
+
+@pytest.mark.parametrize("W,H", [(131072, 30001), (65536, 65535)])
+def test_tail_split_odd_rows(gpu, W, H):
+    """34 strips x 118 256-row bands and 17 x 256: both more than one round of
+    resident waves, so the planned 10-generation passes end in tail bands."""
+    _run(W, H, 20, seed=H)
