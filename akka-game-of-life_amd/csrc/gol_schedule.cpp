@@ -145,8 +145,10 @@ int pick_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int64_t re
 // band (scripts/small_sweep.py, profiles/r06_small_sweep.txt, us per
 // generation, unhashed): 4096^2 14.4 -> 2.3 at G = 10 in 4-row bands, 8192^2
 // 14.4 -> 3.1-3.3, 16384^2 14.3 -> 5.3, 32768^2 18.1 -> 11.9; G = 10 stays the
-// best depth (or within 3 % of it) at every size, hashed or not.  Returns the
-// band, or 0 when the board fills the GPU (the rules above stand).
+// best depth (or within 3 % of it) at every size, hashed or not, so the
+// planner plans hashed passes on these boards with the unhashed cost row
+// (small_board below).  Returns the band, or 0 when the board fills the GPU
+// (the rules above stand).
 int small_board_band(const gol_ctx* ctx, int64_t rows, int strips, int gens, int band, int64_t resident) {
     if (ctx->band_rows > 0 || gens <= 1 || resident <= 0 || strips <= 0 || band <= 0) return 0;
     const int64_t waves = (rows + band - 1) / band * strips;
