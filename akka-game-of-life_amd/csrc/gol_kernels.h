@@ -98,6 +98,7 @@ struct StepParams {
     int32_t strips;            // column strips per row
     int32_t wrap_x;            // torus in x
     int32_t wrap_y;            // unsharded torus: local rows wrap modulo `rows`
+    int32_t whole_row;         // one strip = the whole torus row (kWholeRow*: wave-rotate neighbours, no halo lanes)
     int64_t halo_stride;       // words between halo rows (0: one row repeated)
     uint32_t birth;
     uint32_t survive;
@@ -114,6 +115,18 @@ constexpr int kClockSlotWords = kClockSubSlots * kClockSubWords;
 
 // Strip geometry of a launch: words covered per wave.
 int strip_words(int vec, int gens);
+
+// Whole-row waves: a B3/S23 torus in the pair layout whose row is exactly one
+// wave of 2-word lanes (64 pairs, 4096 columns -- BASELINE.json configs[1])
+// runs its kWholeRowGens-deep passes as one strip without halo lanes: the
+// lane-edge words come from a wave rotate, so every lane is an output lane
+// and the row takes one wave per band instead of two (62 + 2 pairs).
+constexpr int kWholeRowGens = 10;
+constexpr int kWholeRowVec = 2;
+inline bool whole_row_fits(int vec, int gens, bool life, bool clipped, int ilv, bool torus, int64_t wwords) {
+    return torus && life && !clipped && ilv == 2 && vec == kWholeRowVec && gens == kWholeRowGens &&
+           wwords == (int64_t)kWaveLanes * kWholeRowVec;
+}
 
 // vec: words per lane (1, 2 or 4); gens: generations per pass; life: B3/S23
 // fast path (torus only); hash: fuse the per-generation state hash; clipped:

@@ -331,12 +331,14 @@ int launch_ranges(gol_ctx* ctx, int gens, const uint32_t* cur, uint32_t* nxt, co
     p.wwords = ctx->wwords;
     p.rows = geom ? geom->rows : (int32_t)ctx->rows;
     const int vec = lane_words(ctx, gens);
-    const int sw = gol::strip_words(vec, gens);
+    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
+    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
+    p.whole_row = gol::whole_row_fits(vec, gens, life, clipped, ctx->ilv, ctx->topology == GOL_TORUS, ctx->wwords)
+                      ? 1 : 0;
+    const int sw = p.whole_row ? gol::kWaveLanes * vec : gol::strip_words(vec, gens);
     p.strips = (int32_t)((ctx->wwords + sw - 1) / sw);
     int64_t maxlen = 0;
     for (int k = 0; k < n; ++k) maxlen = std::max<int64_t>(maxlen, hi[k] - lo[k]);
-    const bool clipped = ctx->topology == GOL_REF_CLIPPED;
-    const bool life = !clipped && ctx->birth == GOL_RULE_LIFE_BIRTH && ctx->survive == GOL_RULE_LIFE_SURVIVE;
     const int64_t resident = (n == 1 && gens > 1) ? resident_waves(ctx, vec, gens, life, slots != nullptr, clipped) : 0;
     int band = pick_band(ctx, maxlen, p.strips, gens, resident);
     const int small = n == 1 ? small_board_band(ctx, maxlen, p.strips, gens, band, resident) : 0;

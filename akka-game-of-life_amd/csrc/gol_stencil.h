@@ -53,6 +53,8 @@ static_assert(kMRing % 6 == 0, "the paired-row schedule reads a row's parity fro
                                   "the stage rings index slots mod 3");
 constexpr int kDppWaveShr1 = 0x138;  // lane i <- lane i-1 (lane 0 keeps `old`)
 constexpr int kDppWaveShl1 = 0x130;  // lane i <- lane i+1 (lane 63 keeps `old`)
+constexpr int kDppWaveRol1 = 0x134;  // lane i <- lane i+1, lane 63 <- lane 0
+constexpr int kDppWaveRor1 = 0x13C;  // lane i <- lane i-1, lane 0 <- lane 63
 
 // f(integral_constant<int, 0>), ..., f(integral_constant<int, N-1>): a loop
 // whose index is a compile-time constant in every copy, whatever the
@@ -83,6 +85,13 @@ __device__ __forceinline__ uint32_t dpp_shr1_zero(uint32_t v) {
 }
 __device__ __forceinline__ uint32_t dpp_shl1_zero(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppWaveShl1, 0xf, 0xf, true);
+}
+// Wave rotates (whole-row waves: the row wraps inside the wave).
+__device__ __forceinline__ uint32_t dpp_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppWaveRor1, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_rol1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kDppWaveRol1, 0xf, 0xf, false);
 }
 
 // Bits [0, limit) of word `w` set (limit in cells).
@@ -848,7 +857,7 @@ struct HRow {
     uint32_t a[CLIPPED ? VEC : 1];       // clipped: the real row (alive bits)
 };
 
-template <int VEC, bool CLIPPED, int ILV>
+template <int VEC, bool CLIPPED, int ILV, bool WR = false>
 __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const uint32_t (&cmask)[VEC],
                                        HRow<VEC, CLIPPED>& o) {
     uint32_t rv[VEC];
@@ -857,8 +866,9 @@ __device__ __forceinline__ void arrive(const Words<VEC>& raw, bool vis, const ui
         rv[j] = CLIPPED ? (vis ? (raw.w[j] & cmask[j]) : 0u) : raw.w[j];
         if constexpr (CLIPPED) o.a[j] = raw.w[j];
     }
-    const uint32_t left = dpp_shr1_zero(rv[VEC - 1]);  // halo lanes read zeros at the wave's ends
-    const uint32_t right = dpp_shl1_zero(rv[0]);
+    // halo lanes read zeros at the wave's ends; a whole-row wave wraps
+    const uint32_t left = WR ? dpp_ror1(rv[VEC - 1]) : dpp_shr1_zero(rv[VEC - 1]);
+    const uint32_t right = WR ? dpp_rol1(rv[0]) : dpp_shl1_zero(rv[0]);
     static_assert(ILV == 1 || !CLIPPED, "clipped boards are row-major");
 #pragma unroll
     for (int j = 0; j < VEC; ++j) {  // interleaved groups: see rule_words
@@ -919,12 +929,16 @@ __device__ __forceinline__ void rule_hg(const StepParams& p, const HRow<VEC, CLI
 template <int VEC, bool LIFE, bool CLIPPED>
 constexpr bool kPairRows = LIFE && !CLIPPED && VEC <= 2;
 
-template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV>
+// WR: a whole-row wave (gol_kernels.h whole_row_fits) -- 64 output lanes,
+// the row's wrap a wave rotate, one strip.
+template <int VEC, int G, bool LIFE, bool HASH, bool CLIPPED, int ILV, bool WR = false>
 __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(const StepParams p) {
     static_assert(VEC <= 2, "16-byte lanes run the vertical-first kernel");
     static_assert(G >= 2 && G <= kMaxGensPerPass, "G");
     static_assert(G < 32 * VEC, "halo lane narrower than the garbage front");
-    constexpr int kOut = (kWaveLanes - 2) * VEC;
+    static_assert(!WR || (LIFE && !CLIPPED && ILV == 2), "whole-row waves: B3/S23 tori in the pair layout");
+    constexpr int kHaloLanes = WR ? 0 : 1;  // per side
+    constexpr int kOut = (kWaveLanes - 2 * kHaloLanes) * VEC;
     const int lane = threadIdx.x & (kWaveLanes - 1);
     const int wave_in_wg = __builtin_amdgcn_readfirstlane(threadIdx.x / kWaveLanes);
     const WaveTile tile = wave_tile(p, xcd_block(blockIdx.x, gridDim.x, p.xcd_chunk) * kWavesPerWG + wave_in_wg);
@@ -942,8 +956,8 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
         const int n_in = nrows + 2 * G;
         const int s0 = strip * kOut;
         const int nout = min(kOut, p.wwords - s0);
-        const int col = s0 + (lane - 1) * VEC;
-        const bool owns = lane >= 1 && (lane - 1) * VEC < nout;
+        const int col = s0 + (lane - kHaloLanes) * VEC;
+        const bool owns = lane >= kHaloLanes && (lane - kHaloLanes) * VEC < nout;
         // The last strip of a row owns fewer than 62 lanes' words (4 of 62 pairs
         // at 262144 columns, 32 at 65536): lanes past its right halo lane would
         // only compute garbage.  Switch them off -- an exec-masked lane issues
@@ -951,7 +965,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
         // held at its power limit (DESIGN.md §4 "Clock").  DPP reads a
         // switched-off lane as zero (bound_ctrl), as it reads past lane 63.
         // The hashed instances keep every lane: hash_flush reduces across all 64.
-        if constexpr (!HASH) {
+        if constexpr (!HASH && !WR) {
             if (lane > (nout + VEC - 1) / VEC + 1) return;
         }
         int lcol;
@@ -1032,7 +1046,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                 kae[0] = own_q ? ae : 0u;
                 kao[0] = own_q ? ae + kHashOddAdd : 0u;
             }
-            arrive<VEC, CLIPPED, ILV>(in[u], vis(q), cmask, hr[0][u % 3]);
+            arrive<VEC, CLIPPED, ILV, WR>(in[u], vis(q), cmask, hr[0][u % 3]);
 #pragma unroll
             for (int s = 1; s <= G; ++s) {
                 // stages s.. have no valid row yet; a paired stage also runs the
@@ -1066,7 +1080,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
                     hash_row_lds<VEC, ILV>(kae[s], kao[s], o, odd_lane, hsum + (s - 1) * kNP * kWaveLanes);
                 }
                 if (s < G) {
-                    arrive<VEC, CLIPPED, ILV>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
+                    arrive<VEC, CLIPPED, ILV, WR>(o, vis(m), cmask, hr[s][((u - s) % 3 + 3) % 3]);
                 } else {
                     const int r = brow(m);
                     store_row<VEC>(p.nxt + (int64_t)r * p.pitch, own_row, p.wwords * 4, lcol, owns, o);
@@ -1126,8 +1140,14 @@ hipError_t launch_one(const StepParams& p, int gx, int gy, hipStream_t st) {
     } else if constexpr (!kBuilt<VEC, G, LIFE, CLIPPED>) {
         return hipErrorInvalidValue;
     } else if constexpr (VEC <= 2) {
+        if constexpr (VEC == kWholeRowVec && G == kWholeRowGens && LIFE && !CLIPPED && ILV == 2) {
+            if (p.whole_row)
+                return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV, true>, grid, block, st, p);
+        }
+        if (p.whole_row) return hipErrorInvalidValue;  // no whole-row instance (checked by the host layer)
         return launch_kernel(multistep_hg_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     } else {
+        if (p.whole_row) return hipErrorInvalidValue;
         return launch_kernel(multistep_kernel<VEC, G, LIFE, HASH, CLIPPED, ILV>, grid, block, st, p);
     }
 }

@@ -11,6 +11,11 @@ oracle (bit-exact boards and every generation's hash).
 * the small-board band rule's smallest bands (gol_schedule.cpp
   small_board_band) on tori of 1 and 2 strips, at every depth the planner
   picks and a few fixed ones;
+* whole-row waves (gol_kernels.h whole_row_fits: a 4096-column B3/S23 torus
+  at 10-generation passes runs one 64-lane strip whose row wraps by wave
+  rotates): square and odd-height boards, fixed bands from 1 row to more than
+  the board, hashed and not, and as a 1-rank RCCL self-ring (interior and
+  boundary launches);
 * the tail split (gol_schedule.cpp tail_split: the last round of resident
   waves in bands of band / 6 below 768-row bands) on boards of an odd row
   count, so the bulk range ends in a partial band before the tail bands.
@@ -71,3 +76,41 @@ def test_tail_split_odd_rows(gpu, W, H):
     """34 strips x 118 256-row bands and 17 x 256: both more than one round of
     resident waves, so the planned 10-generation passes end in tail bands."""
     _run(W, H, 20, seed=H)
+
+
+@pytest.mark.parametrize("H,band", [(4096, 0), (4096, 1), (4096, 7), (4097, 4), (333, 0), (20, 0), (4096, 5000)])
+def test_whole_row_waves(gpu, H, band):
+    """4096 columns = 128 words = one wave of pairs: every 10-generation pass
+    runs the whole-row instance (the plan is all 10s), against the oracle."""
+    from gameoflife.engine import GolEngine
+    W, gens = 4096, 30
+    board = O.seed_packed(W, H, H + band)
+    for hashed in (False, True):
+        with GolEngine(W, H, topology="torus", rule="life") as e:
+            e.set_tuning(band_rows=band, gens_per_pass=10)
+            e.load(board)
+            got = e.step(gens, hashes=hashed)
+            final_gpu = e.snapshot()
+        final_cpu, want = O.run_packed(board, W, gens, O.TORUS, O.LIFE, nthreads=0)
+        np.testing.assert_array_equal(final_gpu, final_cpu)
+        if hashed:
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, f"first hash mismatch at generation {bad[0] + 1}"
+
+
+def test_whole_row_waves_self_ring(gpu):
+    """The same board as a 1-rank RCCL self-ring: the sharded pass's interior
+    rows and its two boundary row blocks (two row ranges in one launch) both
+    run whole-row waves."""
+    from gameoflife import _native as N
+    from gameoflife.engine import GolEngine
+    W, H, gens = 4096, 512, 40
+    board = O.seed_packed(W, H, 77)
+    with GolEngine(W, H, topology="torus", rule="life") as e:
+        e.comm_init(N.unique_id(), 0, 1)
+        e.load(board)
+        got = e.step(gens, hashes=True)
+        final_gpu = e.snapshot()
+    final_cpu, want = O.run_packed(board, W, gens, O.TORUS, O.LIFE, nthreads=0)
+    np.testing.assert_array_equal(final_gpu, final_cpu)
+    assert (got == want).all()
