@@ -544,6 +544,32 @@ __device__ __forceinline__ void hash_flush(unsigned long long acc, unsigned long
     }
 }
 
+// All G generations of a multi-generation pass at once: the G wave reductions
+// interleaved, one barrier, and workgroup thread s sums and adds generation
+// s (hash_flush once per generation paid 2G barriers per workgroup: on small
+// boards, where a wave streams a few dozen rows, that was a visible share).
+template <int G>
+__device__ __forceinline__ void hash_flush_gens(unsigned long long (&acc)[G], unsigned long long* slots, int lane,
+                                                int wave_in_wg) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int s = 0; s < G; ++s) acc[s] += __shfl_xor(acc[s], off, kWaveLanes);
+    __shared__ unsigned long long part[kWavesPerWG][G];
+    if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < G; ++s) part[wave_in_wg][s] = acc[s];
+    }
+    __syncthreads();
+    const int s = threadIdx.x;
+    if (s < G) {
+        unsigned long long t = 0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerWG; ++w) t += part[w][s];
+        atomicAdd(slots + (size_t)s * kHashGenStride + (size_t)(blockIdx.x % kHashSlots) * kHashSlotStride, t);
+    }
+}
+
 // --------------------------------------------------------------------------
 // One generation per pass.
 // --------------------------------------------------------------------------
@@ -831,8 +857,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_kernel(cons
         }
     }
     if constexpr (HASH) {
-#pragma unroll
-        for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
+        hash_flush_gens<G>(acc, p.hash_slots, lane, wave_in_wg);
     }
     clock_probe_end(p.clk, clk0);
 }
@@ -1117,8 +1142,7 @@ __global__ __launch_bounds__(kWaveLanes* kWavesPerWG) void multistep_hg_kernel(c
         }
     }
     if constexpr (HASH) {
-#pragma unroll
-        for (int s = 0; s < G; ++s) hash_flush(acc[s], p.hash_slots + (size_t)s * kHashGenStride, lane, wave_in_wg);
+        hash_flush_gens<G>(acc, p.hash_slots, lane, wave_in_wg);
     }
     clock_probe_end(p.clk, clk0);
 }
