@@ -118,6 +118,17 @@ __global__ void hash_kernel(const uint32_t* plane, int64_t pitch, int32_t wwords
 // out[64..127]  = dpp wave_shl:1 (old = 0xB0B0B0B0) of in[lane]
 // out[128..191] = alignbit(in[lane], in[(lane+63)%64], 31)
 // out[192..255] = in[5] via a wave-uniform scalar load
+// folded[g] = the sum of generation g's kHashSlots accumulators (mod 2^64).
+__global__ void fold_kernel(const unsigned long long* slots, uint32_t gens, unsigned long long* folded) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= gens) return;
+    const unsigned long long* s = slots + (size_t)g * kHashGenStride;
+    unsigned long long h = 0;
+#pragma unroll 8
+    for (int k = 0; k < kHashSlots; ++k) h += s[(size_t)k * kHashSlotStride];
+    folded[g] = h;  // vector store
+}
+
 __global__ void selftest_kernel(const uint32_t* in, uint32_t* out) {
     const int lane = threadIdx.x;
     const uint32_t v = in[lane];
@@ -194,6 +205,12 @@ hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int
     if (ilv != 1 && ilv != 2) return hipErrorInvalidValue;
     return launch_kernel(hash_kernel, dim3(blocks), dim3(256), stream, plane, pitch, wwords, grow0, rows, ilv,
                          slots);
+}
+
+hipError_t launch_fold(const unsigned long long* slots, uint32_t gens, unsigned long long* folded,
+                       hipStream_t stream) {
+    if (gens == 0) return hipSuccess;
+    return launch_kernel(fold_kernel, dim3((gens + 255) / 256), dim3(256), stream, slots, gens, folded);
 }
 
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream) {

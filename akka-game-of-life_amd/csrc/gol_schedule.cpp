@@ -252,7 +252,9 @@ int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     ctx->slots = ctx->host_slots = nullptr;
     if (old_dev) HIP_CHECK(ctx, hipFree(old_dev));
     if (old_host) HIP_CHECK(ctx, hipHostFree(old_host));
-    const size_t n = (size_t)gens * gol::kHashSlots * gol::kHashSlotStride;
+    // per generation kHashGenStride accumulators, then one folded sum per
+    // generation (gol::launch_fold) at slots + gens * kHashGenStride
+    const size_t n = (size_t)gens * gol::kHashGenStride + gens;
     HIP_CHECK(ctx, hipMalloc(&ctx->slots, n * sizeof(unsigned long long)));
     HIP_CHECK(ctx, hipHostMalloc((void**)&ctx->host_slots, n * sizeof(unsigned long long), hipHostMallocDefault));
     ctx->slots_gens = gens;  // only once both buffers exist
