@@ -369,11 +369,6 @@ int gol_load(gol_ctx* ctx, const uint32_t* packed, int64_t host_pitch_words) {
     return GOL_OK;
 }
 
-// Hashed chunks of at least this many generations fold their accumulators on
-// the device (one more launch, 4 KiB less readback per generation); shorter
-// ones -- a NextStep tick's step(1) -- read the accumulators back whole.
-constexpr uint32_t kDeviceFoldGens = 32;
-
 int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
     if (!ctx) return set_err(nullptr, GOL_EINVAL, "null context");
     if (int rc = bind(ctx)) return rc;
@@ -395,20 +390,7 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
             if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
             g += (uint32_t)G;
         }
-        if (n >= kDeviceFoldGens) {
-            // fold on the device: 8 bytes per generation cross PCIe, not 4 KiB
-            const size_t off = (size_t)ctx->slots_gens * per;
-            HIP_CHECK(ctx, gol::launch_fold(ctx->slots, n, ctx->slots + off, ctx->compute));
-            HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots + off, ctx->slots + off, n * sizeof(unsigned long long),
-                                          hipMemcpyDeviceToHost, ctx->compute));
-            HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-            std::memcpy(hashes_out + g0, ctx->host_slots + off, n * sizeof(uint64_t));
-            continue;
-        }
-        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, n * per * sizeof(unsigned long long),
-                                      hipMemcpyDeviceToHost, ctx->compute));
-        HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-        fold_slots(ctx, n, hashes_out + g0);
+        if (int rc = read_hashes(ctx, n, hashes_out + g0)) return rc;
     }
     return GOL_OK;
 }

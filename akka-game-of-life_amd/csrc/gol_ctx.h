@@ -179,6 +179,9 @@ void destroy_impl(gol_ctx* c);
 
 int ensure_slots(gol_ctx* ctx, uint32_t gens);
 void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out);
+// After the chunk's passes on the compute stream: its `gens` generations'
+// hashes into out[] (device-side fold for long chunks), synchronising.
+int read_hashes(gol_ctx* ctx, uint32_t gens, uint64_t* out);
 int lane_words(const gol_ctx* ctx, int gens);
 int64_t resident_waves(const gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped);
 // Load every step kernel instance the context can launch at its current

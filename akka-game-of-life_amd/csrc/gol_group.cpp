@@ -192,11 +192,7 @@ int gol_group_step_partials(gol_group* g, uint32_t generations, uint64_t* hashes
             for (int k = 0; k < n; ++k) {
                 gol_ctx* s = g->shards[k];
                 if (int rc = bind(s)) return group_fail(g, s, rc);
-                hipError_t e = hipMemcpyAsync(s->host_slots, s->slots, cnt * per * sizeof(unsigned long long),
-                                              hipMemcpyDeviceToHost, s->compute);
-                if (e == hipSuccess) e = hipStreamSynchronize(s->compute);
-                if (e != hipSuccess) return group_fail(g, s, hip_fail(s, e, "hash readback", __FILE__, __LINE__));
-                fold_slots(s, cnt, part.data());
+                if (int rc = read_hashes(s, cnt, part.data())) return group_fail(g, s, rc);
                 for (uint32_t j = 0; j < cnt; ++j) hashes_out[g0 + j] += part[j];
                 if (partials_out)
                     std::copy(part.begin(), part.end(), partials_out + (size_t)k * generations + g0);

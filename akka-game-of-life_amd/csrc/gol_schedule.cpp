@@ -261,6 +261,29 @@ int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     return GOL_OK;
 }
 
+// Hashed chunks of at least this many generations fold their accumulators on
+// the device (one more launch, 4 KiB less readback per generation: configs[1]
+// hashed 1.96 -> 1.73 ms, profiles/r06_device_fold_4096.txt); shorter ones --
+// a NextStep tick's step(1) -- read the accumulators back whole.
+constexpr uint32_t kDeviceFoldGens = 32;
+
+int read_hashes(gol_ctx* ctx, uint32_t gens, uint64_t* out) {
+    if (gens >= kDeviceFoldGens) {
+        const size_t off = (size_t)ctx->slots_gens * gol::kHashGenStride;  // the folded sums (ensure_slots)
+        HIP_CHECK(ctx, gol::launch_fold(ctx->slots, gens, ctx->slots + off, ctx->compute));
+        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots + off, ctx->slots + off, gens * sizeof(unsigned long long),
+                                      hipMemcpyDeviceToHost, ctx->compute));
+        HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+        std::memcpy(out, ctx->host_slots + off, gens * sizeof(uint64_t));
+        return GOL_OK;
+    }
+    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, gens * gol::kHashGenStride * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, ctx->compute));
+    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
+    fold_slots(ctx, gens, out);
+    return GOL_OK;
+}
+
 // Sum the kHashSlots accumulators of each generation (mod 2^64).
 void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out) {
     for (uint32_t g = 0; g < gens; ++g) {
