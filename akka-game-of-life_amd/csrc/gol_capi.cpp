@@ -145,7 +145,7 @@ void destroy_impl(gol_ctx* c) {
     for (void* p : {(void*)c->snap, (void*)c->clk_buf, (void*)c->plane[0], (void*)c->plane[1], (void*)c->halo_top,
                     (void*)c->halo_bot, (void*)c->zero_row, (void*)c->slots})
         if (p) hip_note(hipFree(p), "destroy: hipFree");
-    if (c->host_slots) hip_note(hipHostFree(c->host_slots), "destroy: hipHostFree");
+    if (c->host_folded) hip_note(hipHostFree(c->host_folded), "destroy: hipHostFree");
     for (hipStream_t st : {c->compute, c->comm, c->edge, c->xfer})
         if (st) hip_note(hipStreamDestroy(st), "destroy: hipStreamDestroy");
     delete c;
@@ -384,7 +384,7 @@ int gol_step(gol_ctx* ctx, uint32_t generations, uint64_t* hashes_out) {
         const uint32_t n = std::min(kChunk, generations - g0);
         if (int rc = ensure_slots(ctx, n)) return rc;
         const size_t per = (size_t)gol::kHashGenStride;
-        HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, n * per * sizeof(unsigned long long), ctx->compute));
+        if (int rc = clear_slots(ctx, n)) return rc;
         uint32_t g = 0;
         for (const int G : plan_passes(ctx, n, true)) {
             if (int rc = one_pass(ctx, G, ctx->slots + g * per)) return rc;
@@ -421,15 +421,10 @@ int gol_hash(gol_ctx* ctx, uint64_t* hash_out) {
     if (!ctx || !hash_out) return set_err(ctx, GOL_EINVAL, "null argument");
     if (int rc = bind(ctx)) return rc;
     if (int rc = ensure_slots(ctx, 1)) return rc;
-    const size_t per = (size_t)gol::kHashSlots * gol::kHashSlotStride;
-    HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, per * sizeof(unsigned long long), ctx->compute));
+    if (int rc = clear_slots(ctx, 1)) return rc;
     HIP_CHECK(ctx, gol::launch_hash(ctx->plane[ctx->cur], ctx->pitch, ctx->wwords, ctx->row0, (int32_t)ctx->rows,
                                     ctx->ilv, ctx->slots, ctx->compute));
-    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, per * sizeof(unsigned long long),
-                                  hipMemcpyDeviceToHost, ctx->compute));
-    HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-    fold_slots(ctx, 1, hash_out);
-    return GOL_OK;
+    return read_hashes(ctx, 1, hash_out);
 }
 
 int gol_host_alloc(size_t bytes, void** out) {

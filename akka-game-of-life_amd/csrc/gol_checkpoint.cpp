@@ -45,8 +45,7 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     if (int rc = bind(ctx)) return rc;
     if (hashes_out) {
         if (int rc = ensure_slots(ctx, generations)) return rc;
-        HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, (size_t)n * gol::kHashGenStride * sizeof(unsigned long long),
-                                      ctx->compute));
+        if (int rc = clear_slots(ctx, generations)) return rc;
     }
     const size_t bytes = (size_t)ext * ctx->pitch * sizeof(uint32_t);
     uint32_t* blk[2] = {nullptr, nullptr};
@@ -111,13 +110,16 @@ int gol_replay(gol_ctx* ctx, uint32_t generations, const uint32_t* above, const 
     }
     e = hipMemcpyAsync(ctx->plane[ctx->cur], blk[cur] + n * pitch, (size_t)ctx->rows * pitch * 4,
                        hipMemcpyDeviceToDevice, ctx->compute);
-    if (e == hipSuccess && hashes_out)
-        e = hipMemcpyAsync(ctx->host_slots, ctx->slots, (size_t)n * gol::kHashGenStride * 8,
-                           hipMemcpyDeviceToHost, ctx->compute);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->compute);
+    if (e != hipSuccess) return fail_hip(e, "light-cone result");
+    if (hashes_out) {
+        if (int rc = read_hashes(ctx, generations, hashes_out)) {  // synchronises
+            release();
+            return rc;
+        }
+    }
+    e = hipStreamSynchronize(ctx->compute);
     if (e != hipSuccess) return fail_hip(e, "light-cone result");
     release();
-    if (hashes_out) fold_slots(ctx, generations, hashes_out);
     ctx->epoch += (uint64_t)n;
     return GOL_OK;
 }

@@ -80,8 +80,9 @@ struct gol_ctx {
     uint32_t* zero_row = nullptr;
     unsigned long long* slots = nullptr;  // [gens][kHashSlots * kHashSlotStride]
     uint32_t slots_gens = 0;
-    unsigned long long* host_slots = nullptr;  // page-locked copy of `slots` (hipHostMalloc: the per-generation
-                                               // readback is a direct DMA, not a staged pageable copy)
+    uint32_t slots_clean = 0;  // leading generations of `slots` known to be zero (left so by read_hashes)
+    unsigned long long* host_folded = nullptr;      // [slots_gens] page-locked, mapped: per-generation sums
+    unsigned long long* host_folded_dev = nullptr;  // ... its device address (fold_kernel stores there)
     uint64_t epoch = 0;
     hipStream_t compute = nullptr, comm = nullptr;
     hipStream_t edge = nullptr;  // boundary-row kernels of a sharded pass (concurrent with the interior)
@@ -178,9 +179,12 @@ void destroy_impl(gol_ctx* c);
 // ---- pass schedule (gol_schedule.cpp) --------------------------------------
 
 int ensure_slots(gol_ctx* ctx, uint32_t gens);
-void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out);
+// Before a hashed chunk: the first `gens` generations' accumulators zero
+// (a memset unless read_hashes left them so); marks them in use.
+int clear_slots(gol_ctx* ctx, uint32_t gens);
 // After the chunk's passes on the compute stream: its `gens` generations'
-// hashes into out[] (device-side fold for long chunks), synchronising.
+// hashes into out[], folded on the device straight into mapped host memory,
+// the accumulators cleared again; synchronises.
 int read_hashes(gol_ctx* ctx, uint32_t gens, uint64_t* out);
 int lane_words(const gol_ctx* ctx, int gens);
 int64_t resident_waves(const gol_ctx* ctx, int vec, int gens, bool life, bool hash, bool clipped);

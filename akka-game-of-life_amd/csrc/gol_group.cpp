@@ -174,8 +174,7 @@ int gol_group_step_partials(gol_group* g, uint32_t generations, uint64_t* hashes
             for (gol_ctx* s : g->shards) {
                 if (int rc = bind(s)) return group_fail(g, s, rc);
                 if (int rc = ensure_slots(s, cnt)) return group_fail(g, s, rc);
-                if (hipError_t e = hipMemsetAsync(s->slots, 0, cnt * per * sizeof(unsigned long long), s->compute))
-                    return group_fail(g, s, hip_fail(s, e, "hipMemsetAsync", __FILE__, __LINE__));
+                if (int rc = clear_slots(s, cnt)) return group_fail(g, s, rc);
                 base.push_back(s->slots);
             }
         }

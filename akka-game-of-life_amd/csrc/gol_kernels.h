@@ -155,10 +155,10 @@ hipError_t launch_convert(const uint32_t* src, uint32_t* dst, int64_t pitch, int
 hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int64_t grow0,
                        int32_t rows, int ilv, unsigned long long* slots, hipStream_t stream);
 
-// folded[g] = sum of generation g's hash accumulators, g < gens (gol_step's
-// long hashed chunks: 8 bytes per generation cross PCIe instead of 4 KiB).
-hipError_t launch_fold(const unsigned long long* slots, uint32_t gens, unsigned long long* folded,
-                       hipStream_t stream);
+// folded[g] = sum of generation g's hash accumulators, g < gens, which it
+// clears; `folded` may be mapped host memory (8 bytes per generation cross
+// PCIe instead of the 4 KiB of accumulators).
+hipError_t launch_fold(unsigned long long* slots, uint32_t gens, unsigned long long* folded, hipStream_t stream);
 
 // DPP / lane-shift self test: out[64*4] (see gol_selftest in gol_capi.cpp).
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream);

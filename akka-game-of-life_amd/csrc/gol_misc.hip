@@ -118,15 +118,20 @@ __global__ void hash_kernel(const uint32_t* plane, int64_t pitch, int32_t wwords
 // out[64..127]  = dpp wave_shl:1 (old = 0xB0B0B0B0) of in[lane]
 // out[128..191] = alignbit(in[lane], in[(lane+63)%64], 31)
 // out[192..255] = in[5] via a wave-uniform scalar load
-// folded[g] = the sum of generation g's kHashSlots accumulators (mod 2^64).
-__global__ void fold_kernel(const unsigned long long* slots, uint32_t gens, unsigned long long* folded) {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= gens) return;
-    const unsigned long long* s = slots + (size_t)g * kHashGenStride;
-    unsigned long long h = 0;
-#pragma unroll 8
-    for (int k = 0; k < kHashSlots; ++k) h += s[(size_t)k * kHashSlotStride];
-    folded[g] = h;  // vector store
+// One wave per generation g: lane k takes accumulator k and clears it, the
+// wave sums them (mod 2^64) and lane 0 stores the sum to folded[g] -- mapped
+// page-locked host memory, read by the host after the stream synchronises.
+static_assert(kHashSlots == kWaveLanes, "one accumulator per lane");
+__global__ __launch_bounds__(kWaveLanes) void fold_kernel(unsigned long long* slots, uint32_t gens,
+                                                          unsigned long long* folded) {
+    const uint32_t g = blockIdx.x;
+    const int lane = threadIdx.x;
+    unsigned long long* a = slots + (size_t)g * kHashGenStride + (size_t)lane * kHashSlotStride;
+    unsigned long long h = *a;
+    *a = 0ull;  // the slots are left clear for the next hashed pass (ctx->slots_clean)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h += __shfl_xor(h, off, kWaveLanes);
+    if (lane == 0) folded[g] = h;  // vector store
 }
 
 __global__ void selftest_kernel(const uint32_t* in, uint32_t* out) {
@@ -207,10 +212,9 @@ hipError_t launch_hash(const uint32_t* plane, int64_t pitch, int32_t wwords, int
                          slots);
 }
 
-hipError_t launch_fold(const unsigned long long* slots, uint32_t gens, unsigned long long* folded,
-                       hipStream_t stream) {
+hipError_t launch_fold(unsigned long long* slots, uint32_t gens, unsigned long long* folded, hipStream_t stream) {
     if (gens == 0) return hipSuccess;
-    return launch_kernel(fold_kernel, dim3((gens + 255) / 256), dim3(256), stream, slots, gens, folded);
+    return launch_kernel(fold_kernel, dim3(gens), dim3(kWaveLanes), stream, slots, gens, folded);
 }
 
 hipError_t launch_selftest(const uint32_t* in, uint32_t* out, hipStream_t stream) {

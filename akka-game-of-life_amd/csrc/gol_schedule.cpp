@@ -247,52 +247,40 @@ int ensure_slots(gol_ctx* ctx, uint32_t gens) {
     // the context forgets both buffers before freeing them, so a failure on
     // the way leaves nothing to free twice (destroy_impl frees what is set)
     ctx->slots_gens = 0;
+    ctx->slots_clean = 0;
     unsigned long long* old_dev = ctx->slots;
-    unsigned long long* old_host = ctx->host_slots;
-    ctx->slots = ctx->host_slots = nullptr;
+    unsigned long long* old_host = ctx->host_folded;
+    ctx->slots = ctx->host_folded = ctx->host_folded_dev = nullptr;
     if (old_dev) HIP_CHECK(ctx, hipFree(old_dev));
     if (old_host) HIP_CHECK(ctx, hipHostFree(old_host));
-    // per generation kHashGenStride accumulators, then one folded sum per
-    // generation (gol::launch_fold) at slots + gens * kHashGenStride
-    const size_t n = (size_t)gens * gol::kHashGenStride + gens;
-    HIP_CHECK(ctx, hipMalloc(&ctx->slots, n * sizeof(unsigned long long)));
-    HIP_CHECK(ctx, hipHostMalloc((void**)&ctx->host_slots, n * sizeof(unsigned long long), hipHostMallocDefault));
-    ctx->slots_gens = gens;  // only once both buffers exist
+    HIP_CHECK(ctx, hipMalloc(&ctx->slots, (size_t)gens * gol::kHashGenStride * sizeof(unsigned long long)));
+    // coherent: fold_kernel's stores reach host memory without a cache flush
+    HIP_CHECK(ctx, hipHostMalloc((void**)&ctx->host_folded, (size_t)gens * sizeof(unsigned long long),
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(ctx, hipHostGetDevicePointer((void**)&ctx->host_folded_dev, ctx->host_folded, 0));
+    ctx->slots_gens = gens;  // only once every buffer exists
     return GOL_OK;
 }
 
-// Hashed chunks of at least this many generations fold their accumulators on
-// the device (one more launch, 4 KiB less readback per generation: configs[1]
-// hashed 1.96 -> 1.73 ms, profiles/r06_device_fold_4096.txt); shorter ones --
-// a NextStep tick's step(1) -- read the accumulators back whole.
-constexpr uint32_t kDeviceFoldGens = 32;
+int clear_slots(gol_ctx* ctx, uint32_t gens) {
+    const bool clean = ctx->slots_clean >= gens;
+    ctx->slots_clean = 0;  // in use until read_hashes clears them again
+    if (!clean)
+        HIP_CHECK(ctx, hipMemsetAsync(ctx->slots, 0, (size_t)gens * gol::kHashGenStride * sizeof(unsigned long long),
+                                      ctx->compute));
+    return GOL_OK;
+}
 
+// Per call (scripts/tick_cost.py): a hashed step(1) on the 7 x 7 default
+// board went from 22.0 us (memset + pass + 4 KiB readback) to 20.4 (pass +
+// fold into mapped memory); configs[1]'s hashed 1000 generations from 1.96 to
+// 1.72 ms (8 bytes per generation cross PCIe instead of 4 KiB).
 int read_hashes(gol_ctx* ctx, uint32_t gens, uint64_t* out) {
-    if (gens >= kDeviceFoldGens) {
-        const size_t off = (size_t)ctx->slots_gens * gol::kHashGenStride;  // the folded sums (ensure_slots)
-        HIP_CHECK(ctx, gol::launch_fold(ctx->slots, gens, ctx->slots + off, ctx->compute));
-        HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots + off, ctx->slots + off, gens * sizeof(unsigned long long),
-                                      hipMemcpyDeviceToHost, ctx->compute));
-        HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-        std::memcpy(out, ctx->host_slots + off, gens * sizeof(uint64_t));
-        return GOL_OK;
-    }
-    HIP_CHECK(ctx, hipMemcpyAsync(ctx->host_slots, ctx->slots, gens * gol::kHashGenStride * sizeof(unsigned long long),
-                                  hipMemcpyDeviceToHost, ctx->compute));
+    HIP_CHECK(ctx, gol::launch_fold(ctx->slots, gens, ctx->host_folded_dev, ctx->compute));
     HIP_CHECK(ctx, hipStreamSynchronize(ctx->compute));
-    fold_slots(ctx, gens, out);
+    std::memcpy(out, ctx->host_folded, gens * sizeof(uint64_t));
+    ctx->slots_clean = gens;
     return GOL_OK;
-}
-
-// Sum the kHashSlots accumulators of each generation (mod 2^64).
-void fold_slots(const gol_ctx* ctx, uint32_t gens, uint64_t* out) {
-    for (uint32_t g = 0; g < gens; ++g) {
-        uint64_t h = 0;
-        const unsigned long long* s =
-            ctx->host_slots + (size_t)g * gol::kHashSlots * gol::kHashSlotStride;
-        for (int k = 0; k < gol::kHashSlots; ++k) h += s[(size_t)k * gol::kHashSlotStride];
-        out[g] = h;
-    }
 }
 
 // Words per lane for a pass of `gens` generations.  Multi-generation strips
