@@ -67,11 +67,13 @@ def main():
     lines += ["", "bench.py HIP-event numbers from the same run (timed region only) beside the trace:"]
 
     def instance(G, hashed):
-        # multistep_hg_kernel<2, G, LIFE, HASH, torus, ILV = 2> (step_kernel<4, ...> at G = 1)
+        # multistep_hg_kernel<2, G, LIFE, HASH, torus, ILV = 2, not whole-row>
+        # (step_kernel<4, ...> at G = 1); round 5's names lack the last argument
         h = "true" if hashed else "false"
         if G == 1:
             return f"step_kernel<4, true, {h}, false, 2>"
-        return f"multistep_hg_kernel<2, {G}, true, {h}, false, 2>"
+        return f"multistep_hg_kernel<2, {G}, true, {h}, false, 2"
+
 
     # Dispatches in time order.  Round 4's window (bench.py fresh_window):
     # seed, untimed settle passes, seed again, the warm-up pass, the timed
