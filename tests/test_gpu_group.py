@@ -39,6 +39,23 @@ def test_group_torus_matches_oracle(gpu, n, gpp):
         s.close()
 
 
+@pytest.mark.parametrize("n", [2, 5])
+def test_group_whole_row_waves(gpu, n):
+    """A 4096-column torus (one wave of pairs per row): the group's
+    10-generation passes run whole-row waves in every shard's interior and
+    boundary launches."""
+    W, H, gens = 4096, 403, 40
+    shards, g, full = make_group(W, H, n, gpp=10, seed=n)
+    got = g.step(gens, hashes=True)
+    board = g.snapshot()
+    ref, want = O.run_packed(full, W, gens, O.TORUS, O.LIFE)
+    np.testing.assert_array_equal(got, want)
+    assert (board == ref).all()
+    g.close()
+    for s in shards:
+        s.close()
+
+
 @pytest.mark.parametrize("n", [2, 4])
 @pytest.mark.parametrize("gpp", [1, 3, 6])
 def test_group_clipped_matches_oracle(gpu, n, gpp):
