@@ -532,7 +532,11 @@ int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, in
     const int blocks =
         gol::resident_blocks_per_cu(vec, gens_per_pass, life, false, clipped, ctx->ilv);
     if (waves_per_cu) *waves_per_cu = blocks * gol::kWavesPerWG;
-    if (strip_words) *strip_words = gol::strip_words(vec, gens_per_pass);
+    if (strip_words)
+        *strip_words = gol::whole_row_fits(vec, gens_per_pass, life, clipped, ctx->ilv, ctx->topology == GOL_TORUS,
+                                           ctx->wwords)
+                           ? gol::kWaveLanes * vec  // whole-row waves: no halo lanes
+                           : gol::strip_words(vec, gens_per_pass);
     return GOL_OK;
 }
 

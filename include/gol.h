@@ -384,7 +384,8 @@ int gol_pass_plan(gol_ctx* ctx, uint32_t generations, int32_t with_hashes, int32
 
 /* Diagnostic: resident 64-lane waves per CU of the step kernel a pass of
  * `gens_per_pass` generations would launch with the context's current
- * tuning (occupancy API), and the strip width in words. */
+ * tuning (occupancy API), and the strip width in words (a whole row for the
+ * whole-row waves of a 4096-column B3/S23 torus at 10-generation passes). */
 int gol_occupancy(gol_ctx* ctx, int32_t gens_per_pass, int32_t* waves_per_cu, int32_t* strip_words);
 
 /* Diagnostic: runs a one-wave kernel exercising the cross-lane primitives the

@@ -54,8 +54,9 @@ def check_unhashed(W, H, gens, gpp, rule=O.LIFE, seed=0, band=0):
 def test_strip_geometry(gpu):
     """gol_occupancy reports 124-word strips (62 output lanes x 2 words) for
     multi-generation passes on the pair layout, 128 or 256 (64 lanes) for
-    single-generation passes and 62 (one word per lane) where the layout is
-    row-major (odd word count)."""
+    single-generation passes, 62 (one word per lane) where the layout is
+    row-major (odd word count) and 128 for the whole-row waves of a
+    4096-column torus."""
     for words in (8192, 8190):
         with engine(32 * words, 16) as e:
             for g in DEPTHS:
@@ -63,6 +64,8 @@ def test_strip_geometry(gpu):
             assert e.occupancy(1)[1] in (128, 256)
     with engine(32 * 8191, 16) as e:  # odd word count: row-major words
         assert e.occupancy(12)[1] == 62
+    with engine(4096, 16) as e:  # one wave of pairs per row: whole-row waves at G = 10 only
+        assert e.occupancy(10)[1] == 128 and e.occupancy(9)[1] == 124
 
 
 def test_headline_instance_keeps_three_waves(gpu):
